@@ -1,0 +1,105 @@
+/* pntf.h — C ABI of libpntf.so, the MI355X (gfx950) hot path of P-NTFields.
+ *
+ * The reference (yhsong0804/P-NTFields) has no FFI: its hot path is the Python methods of
+ * `NN` / `Model` in models/model_res_sigmoid_multi.py and models/model_res_sigmoid.py.
+ * Each entry point below replaces one of those methods; the Python drop-in modules under
+ * p-ntfields_amd/models/ bind them with ctypes.
+ *
+ * Conventions (all entry points):
+ *   - every array argument is a caller-owned DEVICE pointer (HIP memory on the current
+ *     device), fp32 row-major unless stated, int32 for ids/counts;
+ *   - calls are stream-ordered and asynchronous on `stream` (NULL = legacy default);
+ *   - no internal threads, no allocation: scratch is the caller's `ws` of `ws_bytes`
+ *     (query with pntf_workspace_bytes); a smaller ws lowers the grid, never fails
+ *     unless it holds less than one workgroup's slots;
+ *   - return PNTF_OK (0) or a positive pntf_status; no exceptions cross the ABI;
+ *   - thread-compatible, not thread-safe (pntf_last_error is per thread).
+ *
+ * Shapes: n pairs `xp` (n, 2*dim) = [x_start | x_goal]; `Btab` (n_env, dim, 128) per-env
+ * Fourier matrices B (the multi model's B.npy (3,128); the arm model's B^T);
+ * `env` (n) int32 env id per pair or NULL (all env 0).  dim is 3 or 6.
+ */
+#ifndef PNTF_H_
+#define PNTF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNTF_ABI_VERSION 1
+
+typedef enum {
+  PNTF_OK = 0,
+  PNTF_ERR_ARG = 1,         /* bad shape / null pointer / unsupported dim */
+  PNTF_ERR_WORKSPACE = 2,   /* ws too small for a single workgroup */
+  PNTF_ERR_HIP = 3          /* HIP launch / runtime error (see pntf_last_error) */
+} pntf_status;
+
+/* Gradient flavours for the reverse sweep. */
+#define PNTF_GRAD_EXACT 0            /* == Model.gradient(NN.out) autograd (:890-896)     */
+#define PNTF_GRAD_BACKGRAD_COMPAT 1  /* == NN.out_backgrad incl. its encoder[0] quirk     */
+                                     /*    (model_res_sigmoid_multi.py:402-647, :435-438) */
+
+int pntf_abi_version(void);
+const char* pntf_status_string(int status);
+const char* pntf_last_error(void);
+
+/* Number of floats of the packed weight blob. */
+size_t pntf_packed_floats(void);
+
+/* Pack the 30 state-dict tensors (device pointers, reference state-dict order:
+ * encoder.{0..3}, encoder1.{0..2}, generator.{0..4}, generator1.{0..2}, each .weight then
+ * .bias — NN.__init__, model_res_sigmoid_multi.py:155-175) into `packed`
+ * (pntf_packed_floats() floats).  encoder1.0 is ignored (never used by NN.out, :227). */
+int pntf_pack_weights(const float* const* params, int n_params, float* packed,
+                      hipStream_t stream);
+
+/* Device scratch needed by the gradient/planner entry points for n pairs. */
+size_t pntf_workspace_bytes(int64_t n);
+
+/* τ only: NN.out / Model.Tau (model_res_sigmoid_multi.py:215-259, :1188-1193). tau (n). */
+int pntf_tau(const float* packed, int dim, const float* xp, int64_t n, const float* Btab,
+             const int32_t* env, int32_t n_env, float* tau, hipStream_t stream);
+
+/* τ and ∇τ: NN.out + Model.gradient (mode EXACT), NN.out_grad (same values) or
+ * NN.out_backgrad (mode BACKGRAD_COMPAT).  tau (n), dtau (n, 2*dim). */
+int pntf_tau_grad(const float* packed, int dim, const float* xp, int64_t n,
+                  const float* Btab, const int32_t* env, int32_t n_env, int mode,
+                  float* tau, float* dtau, void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* Path velocity: Model.Gradient (model_res_sigmoid_multi.py:1218-1248; per-row norms).
+ * vel (n, 2*dim) = [v_start | v_goal]; tau (n) optional (may be NULL). */
+int pntf_path_velocity(const float* packed, int dim, const float* xp, int64_t n,
+                       const float* Btab, const int32_t* env, int32_t n_env, int mode,
+                       float* vel, float* tau, void* ws, size_t ws_bytes,
+                       hipStream_t stream);
+
+/* Speed at the goal: Model.Speed (model_res_sigmoid_multi.py:1195-1216). speed (n). */
+int pntf_speed(const float* packed, int dim, const float* xp, int64_t n, const float* Btab,
+               const int32_t* env, int32_t n_env, float* speed, void* ws, size_t ws_bytes,
+               hipStream_t stream);
+
+/* Travel time: Model.TravelTimes (model_res_sigmoid_multi.py:1173-1186). tt (n). */
+int pntf_travel_time(const float* packed, int dim, const float* xp, int64_t n,
+                     const float* Btab, const int32_t* env, int32_t n_env, float* tt,
+                     hipStream_t stream);
+
+/* Batched bidirectional planner = q independent copies of test/gib_plan.py:74-86
+ * (Gibson: step 0.03, tol 0.06, max_iter 500, mode BACKGRAD_COMPAT) or
+ * test/arm_plan.py:140-152 (arm: step 0.015, tol 0.03, max_iter 300, mode EXACT).
+ * A query freezes once |x_goal - x_start| <= tol; the loop body runs at most
+ * max_iter + 1 times.  path (q, max_iter + 2, 2*dim): row 0 = start, frozen rows repeat
+ * the final state; steps (q) = number of updates taken (-1 for an invalid env id). */
+int pntf_plan(const float* packed, int dim, const float* xp0, int64_t q, const float* Btab,
+              const int32_t* env, int32_t n_env, int mode, float step, float tol,
+              int32_t max_iter, float* path, int32_t* steps, void* ws, size_t ws_bytes,
+              hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PNTF_H_ */

@@ -1,0 +1,360 @@
+"""CPU oracle for the P-NTFields τ/∇τ hot path — TEST INFRASTRUCTURE ONLY.
+
+A from-scratch numpy restatement of the reference math (yhsong0804/P-NTFields,
+`models/model_res_sigmoid_multi.py`, `models/model_res_sigmoid.py`, `test/gib_plan.py`,
+`test/arm_plan.py`).  It is the *checker*: only `tests/`, `__graft_entry__.smoke()` and
+`bench.py`'s `cpu_baseline` leg may import it.  The product path (`p-ntfields_amd/`) never
+imports it and fails loudly without its HIP library.
+
+Pinning: the restatement is checked against golden vectors produced by importing the
+reference itself in the build container (`tests/golden/make_goldens.py` →
+`tests/golden/*.npz`; `tests/test_oracle_golden.py`).
+
+Every function computes in `dtype` (float64 by default, float32 for the CPU baseline
+timing) on arrays shaped like the reference's:
+    xp   (N, 2*dim)    [x_start | x_goal]
+    B    (dim, 128) shared, or (n_env, dim, 128) with env (N,) int ids
+    params: dict state-dict key -> array (reference key names)
+"""
+import numpy as np
+
+SCALE = 10.0          # Softplus beta (model_res_sigmoid_multi.py:138-140)
+THRESH = 20.0         # torch Softplus default threshold
+H = 128
+
+# ------------------------------------------------------------------ elementwise (A1)
+
+
+def softplus10(y):
+    """torch.nn.Softplus(beta=10) (model_res_sigmoid_multi.py:140): linear above beta*y>20."""
+    by = SCALE * y
+    with np.errstate(over="ignore"):
+        soft = np.log1p(np.exp(np.minimum(by, THRESH))) / SCALE
+    return np.where(by > THRESH, y, soft)
+
+
+def sig10(y):
+    """sigmoid(10 y) = softplus10' (`sigmoid`, model_res_sigmoid_multi.py:76-78)."""
+    return 0.5 * (1.0 + np.tanh(0.5 * SCALE * y))
+
+
+def sig_out(y):
+    """sigmoid(0.1 y) head (`sigmoid_out`, model_res_sigmoid_multi.py:98-100)."""
+    return 0.5 * (1.0 + np.tanh(0.05 * y))
+
+
+def _lin(x, p, name):
+    """Linear layer y = x W^T + b (torch.nn.Linear; weights stored (out, in))."""
+    return x @ p[name + ".weight"].T + p[name + ".bias"]
+
+
+def cast_params(params, dtype):
+    return {k: np.asarray(v, dtype=dtype) for k, v in params.items()}
+
+
+def _per_point_W(B, env, n, dtype):
+    """W = 2*pi*B per point (input_mapping, model_res_sigmoid_multi.py:186-190)."""
+    B = np.asarray(B, dtype=dtype)
+    w = (2.0 * np.pi) * B
+    if w.ndim == 2:
+        return w, False
+    assert env is not None, "per-env B table needs env ids"
+    return w[np.asarray(env)], True
+
+
+def _proj(x, w, per_point):
+    return np.einsum("nd,ndf->nf", x, w) if per_point else x @ w
+
+
+# ------------------------------------------------------------------ forward (A5)
+
+
+def encoder_forward(p, phi):
+    """Encoder on points (model_res_sigmoid_multi.py:227-234); returns z and saved pre-acts."""
+    y0 = _lin(phi, p, "encoder.0")
+    h = softplus10(y0)
+    saved = {"e0": y0, "blk": []}
+    for i in (1, 2):
+        y1 = _lin(h, p, "encoder.%d" % i)
+        a = softplus10(y1)
+        y2 = _lin(a, p, "encoder1.%d" % i) + h
+        h = softplus10(y2)
+        saved["blk"].append((y1, y2))
+    z = _lin(h, p, "encoder.3")
+    return z, saved
+
+
+def merge(zs, zg):
+    """Smooth max/min over the two endpoints (model_res_sigmoid_multi.py:236-244)."""
+    d = zs - zg
+    c = np.log1p(np.exp(-SCALE * np.abs(d))) / SCALE
+    mx = np.maximum(zs, zg) + c
+    mn = np.minimum(zs, zg) - c
+    return np.concatenate([mx, mn], axis=1), sig10(d)
+
+
+def generator_forward(p, u):
+    """Generator + head (model_res_sigmoid_multi.py:246-255)."""
+    saved = {"blk": []}
+    for i in (0, 1, 2):
+        y1 = _lin(u, p, "generator.%d" % i)
+        a = softplus10(y1)
+        y2 = _lin(a, p, "generator1.%d" % i) + u
+        u = softplus10(y2)
+        saved["blk"].append((y1, y2))
+    y3 = _lin(u, p, "generator.3")
+    v = softplus10(y3)
+    y4 = _lin(v, p, "generator.4")
+    tau = sig_out(y4)
+    saved["g3"] = y3
+    return tau, saved
+
+
+def forward(params, xp, B, env=None, dim=3, dtype=np.float64, keep=False):
+    """NN.out (model_res_sigmoid_multi.py:215-259): tau (N,1)."""
+    p = cast_params(params, dtype)
+    xp = np.asarray(xp, dtype=dtype)
+    n = xp.shape[0]
+    w, per = _per_point_W(B, env, n, dtype)
+    q_s = _proj(xp[:, :dim], w, per)
+    q_g = _proj(xp[:, dim:], w, per)
+    q = np.concatenate([q_s, q_g])
+    phi = np.concatenate([np.sin(q), np.cos(q)], axis=1)
+    z, enc = encoder_forward(p, phi)
+    u, s0 = merge(z[:n], z[n:])
+    tau, gen = generator_forward(p, u)
+    if not keep:
+        return tau
+    return tau, dict(p=p, q=q, w=w, per=per, enc=enc, s0=s0, gen=gen, n=n, dim=dim)
+
+
+# ------------------------------------------------------------------ reverse mode (A6/A7)
+
+
+def tau_grad(params, xp, B, env=None, dim=3, dtype=np.float64, compat=False):
+    """tau and d tau / d xp.
+
+    compat=False: exact reverse mode == Model.gradient(NN.out) (model_res_sigmoid_multi.py:890-896).
+    compat=True : NN.out_backgrad (model_res_sigmoid_multi.py:402-647) including its encoder[0]
+                  quirk, act' evaluated at the *activated* value (:435-438).
+    """
+    tau, st = forward(params, xp, B, env, dim, dtype, keep=True)
+    p, n = st["p"], st["n"]
+    # head + G3 (A9 of appendix A)
+    d = 0.1 * tau * (1.0 - tau)                                   # dactout, :592-593
+    dv = d * p["generator.4.weight"][0][None, :] * sig10(st["gen"]["g3"])
+    du = dv @ p["generator.3.weight"]
+    for i in (2, 1, 0):                                           # :615-618
+        y1, y2 = st["gen"]["blk"][i]
+        dr = du * sig10(y2)
+        da = (dr @ p["generator1.%d.weight" % i]) * sig10(y1)
+        du = da @ p["generator.%d.weight" % i] + dr
+    s0 = st["s0"]
+    s1 = 1.0 - s0
+    dM, dm = du[:, :H], du[:, H:]
+    dz = np.concatenate([s0 * dM + s1 * dm, s1 * dM + s0 * dm])   # :620-627
+    dh = dz @ p["encoder.3.weight"]
+    for i in (2, 1):                                              # :633-636
+        y1, y2 = st["enc"]["blk"][i - 1]
+        dr = dh * sig10(y2)
+        da = (dr @ p["encoder1.%d.weight" % i]) * sig10(y1)
+        dh = da @ p["encoder.%d.weight" % i] + dr
+    y0 = st["enc"]["e0"]
+    act0 = sig10(softplus10(y0)) if compat else sig10(y0)         # quirk :435-438
+    dphi = (dh * act0) @ p["encoder.0.weight"]                    # :639
+    q = st["q"]
+    g = dphi[:, :H] * np.cos(q) - dphi[:, H:] * np.sin(q)         # :419, :640
+    w = st["w"]
+    if st["per"]:
+        ww = np.concatenate([w, w])
+        dp = np.einsum("nf,ndf->nd", g, ww)
+    else:
+        dp = g @ w.T                                              # :641
+    dtau = np.concatenate([dp[:n], dp[n:]], axis=1)               # :643-645
+    return tau, dtau
+
+
+# ------------------------------------------------------------------ epilogues (A9/A10)
+
+
+def path_velocity(xp, tau, dtau, dim=3, row_norm=True):
+    """Model.Gradient formula (model_res_sigmoid_multi.py:1223-1248): [v_s | v_g].
+
+    row_norm=False reproduces the arm model's whole-tensor torch.norm
+    (models/model_res_sigmoid.py:1268,1278), identical for a batch of one."""
+    xp = np.asarray(xp, dtype=dtau.dtype)
+    D = xp[:, dim:] - xp[:, :dim]
+    T0 = np.sqrt(np.sum(D * D, axis=1))
+    t = tau[:, 0]
+    T3 = t * t
+    out = []
+    for sign, dt in ((-1.0, dtau[:, :dim]), (1.0, dtau[:, dim:])):
+        Y1 = (1.0 / (T0 * t))[:, None] * (sign * D)
+        Y2 = (T0 / T3)[:, None] * dt
+        Yp = -(Y1 - Y2)
+        S = np.sqrt(np.sum(Yp * Yp, axis=1))[:, None] if row_norm else np.sqrt(np.sum(Yp * Yp))
+        out.append(Yp / S ** 2)
+    return np.concatenate(out, axis=1)
+
+
+def speed(xp, tau, dtau, dim=3):
+    """Model.Speed (model_res_sigmoid_multi.py:1195-1216), at the goal."""
+    xp = np.asarray(xp, dtype=dtau.dtype)
+    D = xp[:, dim:] - xp[:, :dim]
+    T0 = np.sum(D * D, axis=1)
+    DT1 = dtau[:, dim:]
+    t = tau[:, 0]
+    S = T0 * np.sum(DT1 * DT1, axis=1) - 2 * t * np.sum(DT1 * D, axis=1) + t * t
+    return t * t / np.sqrt(S)
+
+
+def travel_time(xp, tau, dim=3):
+    """Model.TravelTimes (model_res_sigmoid_multi.py:1173-1186)."""
+    xp = np.asarray(xp, dtype=tau.dtype)
+    D = xp[:, dim:] - xp[:, :dim]
+    return np.sqrt(np.sum(D * D, axis=1)) / tau[:, 0]
+
+
+# ------------------------------------------------------------------ Taylor mode (A11)
+
+
+def _taylor_act(y, J, L):
+    """act_laplace (model_res_sigmoid_multi.py:675-691); J, L carry a direction axis 1."""
+    s = sig10(y)
+    ds = SCALE * s * (1.0 - s)
+    return softplus10(y), J * s[:, None], J * J * ds[:, None] + L * s[:, None]
+
+
+def _taylor_lin(x, J, L, p, name, res=None):
+    """linear_laplace (:663-673), optional residual add (:744, :828)."""
+    W, b = p[name + ".weight"], p[name + ".bias"]
+    y, J2, L2 = x @ W.T + b, J @ W.T, L @ W.T
+    if res is not None:
+        y, J2, L2 = y + res[0], J2 + res[1], L2 + res[2]
+    return y, J2, L2
+
+
+def laplace(params, xp, B, env=None, dim=3, dtype=np.float64):
+    """NN.out_laplace (model_res_sigmoid_multi.py:710-848) on flat pairs.
+
+    Returns tau (N,1), dtau (N,2dim), ltau (N,2dim) (diagonal second derivatives)."""
+    p = cast_params(params, dtype)
+    xp = np.asarray(xp, dtype=dtype)
+    n = xp.shape[0]
+    w, per = _per_point_W(B, env, n, dtype)
+    ww = np.concatenate([w, w]) if per else w
+    x = np.concatenate([xp[:, :dim], xp[:, dim:]])
+    q = _proj(x, ww, per)
+    sq, cq = np.sin(q), np.cos(q)
+    if per:
+        wd = ww                                                  # (2n, dim, 128)
+    else:
+        wd = np.broadcast_to(w[None], (2 * n, dim, H))
+    h = np.concatenate([sq, cq], axis=1)                          # input_mapping_laplace :199-213
+    J = np.concatenate([wd * cq[:, None], -wd * sq[:, None]], axis=2)
+    L = np.concatenate([-wd * wd * sq[:, None], -wd * wd * cq[:, None]], axis=2)
+    y, J, L = _taylor_lin(h, J, L, p, "encoder.0")
+    h, J, L = _taylor_act(y, J, L)
+    for i in (1, 2):
+        r = (h, J, L)
+        y, J, L = _taylor_lin(h, J, L, p, "encoder.%d" % i)
+        h, J, L = _taylor_act(y, J, L)
+        y, J, L = _taylor_lin(h, J, L, p, "encoder1.%d" % i, res=r)
+        h, J, L = _taylor_act(y, J, L)
+    z, J, L = _taylor_lin(h, J, L, p, "encoder.3")
+    zs, zg = z[:n], z[n:]
+    Js, Jg, Ls, Lg = J[:n], J[n:], L[:n], L[n:]
+    u, s0 = merge(zs, zg)                                         # :761-766
+    s1 = 1.0 - s0
+    c = SCALE * s0 * s1                                           # :790
+    S0, S1, C = s0[:, None], s1[:, None], c[:, None]
+    Jst = np.concatenate([Js * S0, Js * S1], axis=2)              # start directions :776-786
+    Jgo = np.concatenate([Jg * S1, Jg * S0], axis=2)              # goal directions
+    Lst = np.concatenate([Js * C * Js + Ls * S0, -Js * C * Js + Ls * S1], axis=2)   # :793-811
+    Lgo = np.concatenate([Jg * C * Jg + Lg * S1, -Jg * C * Jg + Lg * S0], axis=2)
+    J = np.concatenate([Jst, Jgo], axis=1)                        # (n, 2dim, 256)
+    L = np.concatenate([Lst, Lgo], axis=1)
+    for i in (0, 1, 2):
+        r = (u, J, L)
+        y, J, L = _taylor_lin(u, J, L, p, "generator.%d" % i)
+        u, J, L = _taylor_act(y, J, L)
+        y, J, L = _taylor_lin(u, J, L, p, "generator1.%d" % i, res=r)
+        u, J, L = _taylor_act(y, J, L)
+    y, J, L = _taylor_lin(u, J, L, p, "generator.3")
+    u, J, L = _taylor_act(y, J, L)
+    y, J, L = _taylor_lin(u, J, L, p, "generator.4")
+    t = sig_out(y)                                                # actout_laplace :693-708
+    dt = 0.1 * t * (1.0 - t)
+    ddt = 0.1 * dt * (1.0 - 2.0 * t)
+    Lo = J * J * ddt[:, None] + L * dt[:, None]
+    Jo = J * dt[:, None]
+    return t, Jo[:, :, 0], Lo[:, :, 0]
+
+
+def eikonal_residual(params, xp, yobs, B, env=None, dim=3, gamma=1e-3, dtype=np.float64):
+    """Model.Loss per-pair residual (model_res_sigmoid_multi.py:914-946).
+
+    Returns tau, dtau, ltau, diff (N,).  The scalar loss_n adds the B regulariser on the
+    caller side (:947)."""
+    tau, dtau, ltau = laplace(params, xp, B, env, dim, dtype)
+    xp = np.asarray(xp, dtype=dtype)
+    yobs = np.asarray(yobs, dtype=dtype)
+    D = xp[:, dim:] - xp[:, :dim]
+    T0 = np.sum(D * D, axis=1)
+    lap0 = ltau[:, :dim].sum(-1)
+    lap1 = ltau[:, dim:].sum(-1)
+    DT0, DT1 = dtau[:, :dim], dtau[:, dim:]
+    t = tau[:, 0]
+    T01 = T0 * np.sum(DT0 * DT0, axis=1)
+    T02 = -2 * t * np.sum(DT0 * D, axis=1)
+    T11 = T0 * np.sum(DT1 * DT1, axis=1)
+    T12 = 2 * t * np.sum(DT1 * D, axis=1)
+    T3 = t * t
+    S0 = T01 - T02 + T3
+    S1 = T11 - T12 + T3
+    yp0 = 1.0 / (np.sqrt(S0) / T3 + gamma * lap0)
+    yp1 = 1.0 / (np.sqrt(S1) / T3 + gamma * lap1)
+    y0, y1 = yobs[:, 0], yobs[:, 1]
+    diff = yp0 / y0 + y0 / yp0 + yp1 / y1 + y1 / yp1 - 4.0
+    return tau, dtau, ltau, diff
+
+
+def loss_n(diff, B_table, n_env, n_per_env):
+    """loss_n (model_res_sigmoid_multi.py:947): sum(diff)/E/n + 0.01 ||B||^2 /E/n."""
+    B = np.asarray(B_table, dtype=np.float64)
+    return float(np.sum(diff) / n_env / n_per_env + 0.01 * np.sum(B * B) / n_env / n_per_env)
+
+
+# ------------------------------------------------------------------ planners (A12/A13)
+
+
+def plan(params, xp0, B, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
+         compat=True, row_norm=True, dtype=np.float64):
+    """Batched bidirectional planner == Q independent copies of the batch-1 loop.
+
+    Gibson (`test/gib_plan.py:74-86`): step 0.03, tol 0.06, cap 500, out_backgrad (compat).
+    Arm   (`test/arm_plan.py:140-152`): step 0.015, tol 0.03, cap 300, autograd (exact).
+    A query freezes once |xg - xs| <= tol; the loop body runs at most max_iter+1 times
+    (`iter>max_iter` break after the increment).  Returns (path (Q, max_iter+2, 2dim) with
+    frozen rows repeated, steps (Q,) int)."""
+    xp = np.array(xp0, dtype=dtype)
+    q = xp.shape[0]
+    cap = max_iter + 1
+    path = np.zeros((q, cap + 1, 2 * dim), dtype=dtype)
+    path[:, 0] = xp
+    steps = np.zeros(q, dtype=np.int32)
+    active = np.linalg.norm(xp[:, dim:] - xp[:, :dim], axis=1) > tol
+    for it in range(cap):
+        if not active.any():
+            path[:, it + 1:] = xp[:, None]
+            break
+        idx = np.nonzero(active)[0]
+        e = None if env is None else np.asarray(env)[idx]
+        tau, dtau = tau_grad(params, xp[idx], B, e, dim, dtype, compat=compat)
+        g = path_velocity(xp[idx], tau, dtau, dim, row_norm=row_norm)
+        xp[idx] = xp[idx] + step * g
+        steps[idx] += 1
+        path[:, it + 1] = xp
+        dis = np.linalg.norm(xp[idx, dim:] - xp[idx, :dim], axis=1)
+        active[idx[dis <= tol]] = False
+    return path, steps

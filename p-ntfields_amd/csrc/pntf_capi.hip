@@ -1,0 +1,242 @@
+// C ABI of libpntf.so (declared in include/pntf.h): argument checks, launch geometry,
+// error reporting.  Device code lives in pntf_field.hip.
+#include <stdio.h>
+#include <string.h>
+
+#include "pntf.h"
+
+#include "pntf_common.h"
+
+// Kernels are compiled one per translation unit (pntf_kernels.hip, PNTF_DIM/PNTF_KIND) so
+// the build parallelises; here they are only declared.
+namespace pntf {
+template <int DIM, int KIND>
+__global__ void field_kernel(FieldArgs a);
+template <int DIM>
+__global__ void plan_kernel(PlanArgs a);
+__global__ void pack_kernel(const float* __restrict__ src, int rows, int cols, int ld,
+                            int trans, float* __restrict__ dst);
+__global__ void copy_kernel(const float* __restrict__ src, int n, float* __restrict__ dst);
+}  // namespace pntf
+
+using namespace pntf;
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char* fmt, const char* detail = "") {
+  snprintf(g_err, sizeof(g_err), fmt, detail);
+  return code;
+}
+
+static int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return PNTF_ERR_HIP;
+  }
+  return PNTF_OK;
+}
+
+static int num_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return 256;
+  return cus;
+}
+
+static constexpr size_t SLOT_BYTES = (size_t)SCRATCH_FLOATS_PER_WAVE * sizeof(float);
+
+// persistent grid: one 4-wave workgroup per CU at most, never more than the tiles need
+static int64_t grid_for(int64_t n) {
+  int64_t ntiles = (n + TILE - 1) / TILE;
+  int64_t wgs = (ntiles + WAVES - 1) / WAVES;
+  int64_t cap = (int64_t)num_cus() * WG_PER_CU;
+  return wgs < cap ? (wgs < 1 ? 1 : wgs) : cap;
+}
+
+static int grid_with_ws(int64_t n, size_t ws_bytes, int64_t* grid) {
+  int64_t g = grid_for(n);
+  int64_t fit = (int64_t)(ws_bytes / (SLOT_BYTES * WAVES));
+  if (fit < 1) return fail(PNTF_ERR_WORKSPACE, "workspace too small (%s)", "need >= 4 slots");
+  *grid = g < fit ? g : fit;
+  return PNTF_OK;
+}
+
+// An empty batch is valid whatever the data pointers are (torch hands out NULL for empty
+// tensors); callers return PNTF_OK right after this check when n == 0.
+static int check_common(const float* packed, int dim, const float* xp, int64_t n,
+                        const float* Btab, int32_t n_env) {
+  if (dim != 3 && dim != 6) return fail(PNTF_ERR_ARG, "dim must be 3 or 6%s");
+  if (n < 0) return fail(PNTF_ERR_ARG, "negative batch%s");
+  if (n == 0) return PNTF_OK;
+  if (!packed || !xp || !Btab) return fail(PNTF_ERR_ARG, "null pointer argument%s");
+  if (n_env < 1) return fail(PNTF_ERR_ARG, "n_env must be >= 1%s");
+  return PNTF_OK;
+}
+
+template <int DIM>
+static void launch_field(int kind, int64_t grid, const FieldArgs& a, hipStream_t s) {
+  dim3 g((unsigned)grid), b(256);
+  switch (kind) {
+    case K_TAU: hipLaunchKernelGGL((field_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
+    case K_TAU_GRAD: hipLaunchKernelGGL((field_kernel<DIM, K_TAU_GRAD>), g, b, 0, s, a); break;
+    case K_VELOCITY: hipLaunchKernelGGL((field_kernel<DIM, K_VELOCITY>), g, b, 0, s, a); break;
+    case K_SPEED: hipLaunchKernelGGL((field_kernel<DIM, K_SPEED>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((field_kernel<DIM, K_TRAVEL>), g, b, 0, s, a); break;
+  }
+}
+
+static int run_field(int kind, const float* packed, int dim, const float* xp, int64_t n,
+                     const float* Btab, const int32_t* env, int32_t n_env, int mode,
+                     float* out0, float* out1, void* ws, size_t ws_bytes, hipStream_t s) {
+  int st = check_common(packed, dim, xp, n, Btab, n_env);
+  if (st) return st;
+  if (mode != PNTF_GRAD_EXACT && mode != PNTF_GRAD_BACKGRAD_COMPAT)
+    return fail(PNTF_ERR_ARG, "unknown gradient mode%s");
+  if (n == 0) return PNTF_OK;
+  if (!out0 || (kind == K_TAU_GRAD && !out1)) return fail(PNTF_ERR_ARG, "null output%s");
+  const bool grad = kind != K_TAU && kind != K_TRAVEL;
+  int64_t grid = grid_for(n);
+  if (grad) {
+    if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
+    st = grid_with_ws(n, ws_bytes, &grid);
+    if (st) return st;
+  }
+  FieldArgs a{packed, xp, Btab, env, n, n_env, mode, out0, out1, (float*)ws};
+  if (dim == 3) launch_field<3>(kind, grid, a, s);
+  else launch_field<6>(kind, grid, a, s);
+  return check_launch("field_kernel");
+}
+
+extern "C" {
+
+int pntf_abi_version(void) { return PNTF_ABI_VERSION; }
+
+const char* pntf_status_string(int status) {
+  switch (status) {
+    case PNTF_OK: return "ok";
+    case PNTF_ERR_ARG: return "invalid argument";
+    case PNTF_ERR_WORKSPACE: return "workspace too small";
+    case PNTF_ERR_HIP: return "HIP runtime error";
+    default: return "unknown status";
+  }
+}
+
+const char* pntf_last_error(void) { return g_err; }
+
+size_t pntf_packed_floats(void) { return (size_t)PACKED_FLOATS; }
+
+size_t pntf_workspace_bytes(int64_t n) {
+  if (n <= 0) n = 1;
+  return (size_t)grid_for(n) * WAVES * SLOT_BYTES;
+}
+
+int pntf_pack_weights(const float* const* params, int n_params, float* packed,
+                      hipStream_t stream) {
+  if (!params || !packed) return fail(PNTF_ERR_ARG, "null pointer argument%s");
+  if (n_params != 30) return fail(PNTF_ERR_ARG, "expected 30 state-dict tensors%s");
+  for (int i = 0; i < 30; ++i)
+    if (i != 8 && i != 9 && !params[i]) return fail(PNTF_ERR_ARG, "null state-dict tensor%s");
+  // state-dict index of each packed matrix (pntf_common.h order) and its shape
+  struct M { int idx, rows, cols, off; };
+  const M mats[] = {
+      {0, 128, 256, OFF_E0},                                  // encoder.0
+      {2, 128, 128, OFF_EBLK + 0 * SZ_E},                     // encoder.1
+      {10, 128, 128, OFF_EBLK + 1 * SZ_E},                    // encoder1.1
+      {4, 128, 128, OFF_EBLK + 2 * SZ_E},                     // encoder.2
+      {12, 128, 128, OFF_EBLK + 3 * SZ_E},                    // encoder1.2
+      {6, 128, 128, OFF_E3},                                  // encoder.3
+      {14, 256, 256, OFF_GBLK + 0 * SZ_G},                    // generator.0
+      {24, 256, 256, OFF_GBLK + 1 * SZ_G},                    // generator1.0
+      {16, 256, 256, OFF_GBLK + 2 * SZ_G},                    // generator.1
+      {26, 256, 256, OFF_GBLK + 3 * SZ_G},                    // generator1.1
+      {18, 256, 256, OFF_GBLK + 4 * SZ_G},                    // generator.2
+      {28, 256, 256, OFF_GBLK + 5 * SZ_G},                    // generator1.2
+      {20, 128, 256, OFF_G3},                                 // generator.3
+  };
+  hipMemsetAsync(packed, 0, sizeof(float) * PACKED_FLOATS, stream);
+  for (int m = 0; m < (int)(sizeof(mats) / sizeof(mats[0])); ++m) {
+    const M& d = mats[m];
+    int64_t cnt = (int64_t)d.rows * d.cols;
+    unsigned blocks = (unsigned)((cnt + 255) / 256);
+    // forward: A = W (rows x cols); backward: A = W^T (cols x rows)
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx], d.rows,
+                       d.cols, d.cols, 0, packed + OFF_FWD + d.off);
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx], d.cols,
+                       d.rows, d.cols, 1, packed + OFF_BWD + d.off);
+  }
+  struct Bc { int idx, n, off; };
+  const Bc bs[] = {
+      {1, 128, B_E0},           {3, 128, B_EBLK + 0},     {11, 128, B_EBLK + 128},
+      {5, 128, B_EBLK + 256},   {13, 128, B_EBLK + 384},  {7, 128, B_E3},
+      {15, 256, B_GBLK + 0},    {25, 256, B_GBLK + 256},  {17, 256, B_GBLK + 512},
+      {27, 256, B_GBLK + 768},  {19, 256, B_GBLK + 1024}, {29, 256, B_GBLK + 1280},
+      {21, 128, B_G3},          {22, 128, B_G4W},         {23, 1, B_G4B}};
+  for (int i = 0; i < (int)(sizeof(bs) / sizeof(bs[0])); ++i)
+    hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(256), 0, stream, params[bs[i].idx], bs[i].n,
+                       packed + OFF_BIAS + bs[i].off);
+  return check_launch("pack_weights");
+}
+
+int pntf_tau(const float* packed, int dim, const float* xp, int64_t n, const float* Btab,
+             const int32_t* env, int32_t n_env, float* tau, hipStream_t stream) {
+  return run_field(K_TAU, packed, dim, xp, n, Btab, env, n_env, 0, tau, nullptr, nullptr, 0,
+                   stream);
+}
+
+int pntf_tau_grad(const float* packed, int dim, const float* xp, int64_t n,
+                  const float* Btab, const int32_t* env, int32_t n_env, int mode, float* tau,
+                  float* dtau, void* ws, size_t ws_bytes, hipStream_t stream) {
+  return run_field(K_TAU_GRAD, packed, dim, xp, n, Btab, env, n_env, mode, tau, dtau, ws,
+                   ws_bytes, stream);
+}
+
+int pntf_path_velocity(const float* packed, int dim, const float* xp, int64_t n,
+                       const float* Btab, const int32_t* env, int32_t n_env, int mode,
+                       float* vel, float* tau, void* ws, size_t ws_bytes,
+                       hipStream_t stream) {
+  return run_field(K_VELOCITY, packed, dim, xp, n, Btab, env, n_env, mode, vel, tau, ws,
+                   ws_bytes, stream);
+}
+
+int pntf_speed(const float* packed, int dim, const float* xp, int64_t n, const float* Btab,
+               const int32_t* env, int32_t n_env, float* speed, void* ws, size_t ws_bytes,
+               hipStream_t stream) {
+  return run_field(K_SPEED, packed, dim, xp, n, Btab, env, n_env, PNTF_GRAD_EXACT, speed,
+                   nullptr, ws, ws_bytes, stream);
+}
+
+int pntf_travel_time(const float* packed, int dim, const float* xp, int64_t n,
+                     const float* Btab, const int32_t* env, int32_t n_env, float* tt,
+                     hipStream_t stream) {
+  return run_field(K_TRAVEL, packed, dim, xp, n, Btab, env, n_env, 0, tt, nullptr, nullptr, 0,
+                   stream);
+}
+
+int pntf_plan(const float* packed, int dim, const float* xp0, int64_t q, const float* Btab,
+              const int32_t* env, int32_t n_env, int mode, float step, float tol,
+              int32_t max_iter, float* path, int32_t* steps, void* ws, size_t ws_bytes,
+              hipStream_t stream) {
+  int st = check_common(packed, dim, xp0, q, Btab, n_env);
+  if (st) return st;
+  if (max_iter < 0) return fail(PNTF_ERR_ARG, "max_iter must be >= 0%s");
+  if (mode != PNTF_GRAD_EXACT && mode != PNTF_GRAD_BACKGRAD_COMPAT)
+    return fail(PNTF_ERR_ARG, "unknown gradient mode%s");
+  if (q == 0) return PNTF_OK;
+  if (!path || !steps) return fail(PNTF_ERR_ARG, "null output%s");
+  if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
+  int64_t grid;
+  st = grid_with_ws(q, ws_bytes, &grid);
+  if (st) return st;
+  PlanArgs a{packed, xp0, Btab, env, q, n_env, mode, step, tol, max_iter, path, steps,
+             (float*)ws};
+  if (dim == 3)
+    hipLaunchKernelGGL((plan_kernel<3>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((plan_kernel<6>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+  return check_launch("plan_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// Shared device-side definitions for the P-NTFields MI355X kernels.
+//
+// Data layout of the fused τ/∇τ kernels ("transposed" MFMA formulation):
+//   * one wave owns a tile of 16 (start, goal) pairs; the pair index is the MFMA column
+//     t = lane & 15, so the four lane groups g = lane >> 4 all belong to the same pair;
+//   * an activation vector of 16*k features is k f32x4 "tiles": lane (t, g) holds feature
+//     rows 4 g + s, s = 0..3, of column t — exactly the C/D layout of
+//     v_mfma_f32_16x16x4_f32, so a layer's output tile is the next layer's B operand with
+//     no data movement (k-step s takes register s; lane group g supplies k = g, i.e. row
+//     4 g + s);
+//   * the weights are the A operand, pre-packed ("fragment order") so that one
+//     global_load_dwordx4 per lane fetches the A operands of the 4 k-steps of one input
+//     tile and each wave-instruction reads 1 KiB contiguous:
+//        P[((ot*KT + kt)*64 + lane)*4 + s] = W[16 ot + (lane & 15)][16 kt + 4 (lane >> 4) + s]
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pntf {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int H = 128;              // hidden width (model_res_sigmoid_multi.py:134)
+constexpr int TILE = 16;            // pairs per wave
+constexpr int WAVES = 4;            // waves per workgroup
+// One wave per SIMD: the kernels need up to 512 VGPRs to stay spill-free.  (At two waves per
+// SIMD (256 VGPRs) hipcc spills MFMA results, and on gfx950 those spill stores read the
+// MFMA destination before its last pass lands: corrupt columns 12-15 of 16x16 tiles under
+// load — DESIGN.md §7.)
+#ifndef PNTF_WAVES_PER_SIMD
+#define PNTF_WAVES_PER_SIMD 1
+#endif
+constexpr int WAVES_PER_SIMD = PNTF_WAVES_PER_SIMD;
+constexpr int WG_PER_CU = WAVES_PER_SIMD;
+constexpr float TWO_PI = 6.283185307179586f;
+
+// ---------------------------------------------------------------- packed weight blob
+// One direction (forward A = W, backward A = W^T) holds 15 matrices in this order.
+constexpr int SZ_E0 = 128 * 256, SZ_E = 128 * 128, SZ_G = 256 * 256, SZ_G3 = 128 * 256;
+constexpr int OFF_E0 = 0;
+constexpr int OFF_EBLK = OFF_E0 + SZ_E0;      // (encoder.1, encoder1.1, encoder.2, encoder1.2)
+constexpr int OFF_E3 = OFF_EBLK + 4 * SZ_E;
+constexpr int OFF_GBLK = OFF_E3 + SZ_E;       // (generator.i, generator1.i) for i = 0..2
+constexpr int OFF_G3 = OFF_GBLK + 6 * SZ_G;
+constexpr int SZ_DIR = OFF_G3 + SZ_G3;
+constexpr int OFF_FWD = 0;
+constexpr int OFF_BWD = SZ_DIR;
+constexpr int OFF_BIAS = 2 * SZ_DIR;
+// bias block (plain order)
+constexpr int B_E0 = 0;
+constexpr int B_EBLK = 128;                   // 4 x 128 in the EBLK order above
+constexpr int B_E3 = B_EBLK + 4 * 128;
+constexpr int B_GBLK = B_E3 + 128;            // 6 x 256 in the GBLK order above
+constexpr int B_G3 = B_GBLK + 6 * 256;
+constexpr int B_G4W = B_G3 + 128;             // generator.4.weight (1 x 128)
+constexpr int B_G4B = B_G4W + 128;            // generator.4.bias (padded to 4)
+constexpr int SZ_BIAS = B_G4B + 4;
+constexpr int PACKED_FLOATS = OFF_BIAS + SZ_BIAS;
+
+// ---------------------------------------------------------------- per-wave scratch (saved σ10)
+// Each saved "tile" is 16 feature rows x 16 pairs = 256 floats, stored lane-major
+// (64 lanes x float4) so every store/load instruction moves 1 KiB contiguous.
+constexpr int T_E0 = 0;                       // 2 cols x 8 tiles
+constexpr int T_EBLK = 16;                    // block b (0,1): +32b: y1 (16 tiles), y2 (16 tiles)
+constexpr int T_S0 = 80;                      // merge switch s0 = σ10(zs - zg), 8 tiles
+constexpr int T_GBLK = 88;                    // block i (0..2): +32i: y1 (16), y2 (16)
+constexpr int T_G3 = 184;                     // 8 tiles
+constexpr int SCRATCH_TILES = 192;
+constexpr int SCRATCH_FLOATS_PER_WAVE = SCRATCH_TILES * 256;
+
+// ---------------------------------------------------------------- kernel arguments
+enum Kind { K_TAU = 0, K_TAU_GRAD = 1, K_VELOCITY = 2, K_SPEED = 3, K_TRAVEL = 4 };
+
+struct FieldArgs {
+  const float* P;        // packed weights
+  const float* xp;       // (n, 2*DIM)
+  const float* Btab;     // (n_env, DIM, 128)
+  const int32_t* env;    // (n) or null
+  int64_t n;
+  int32_t n_env;
+  int32_t compat;
+  float* out0;           // tau / velocity / speed / travel time
+  float* out1;           // dtau (K_TAU_GRAD), tau (K_VELOCITY, optional)
+  float* ws;             // scratch, SCRATCH_FLOATS_PER_WAVE per slot
+};
+
+struct PlanArgs {
+  const float* P;
+  const float* xp0;      // (q, 2*DIM)
+  const float* Btab;
+  const int32_t* env;
+  int64_t q;
+  int32_t n_env;
+  int32_t compat;
+  float step, tol;
+  int32_t max_iter;      // the loop body runs at most max_iter + 1 times
+  float* path;           // (q, max_iter + 2, 2*DIM)
+  int32_t* steps;        // (q)
+  float* ws;
+};
+
+}  // namespace pntf

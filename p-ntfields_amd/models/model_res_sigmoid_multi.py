@@ -1,0 +1,222 @@
+"""Drop-in replacement of yhsong0804/P-NTFields `models/model_res_sigmoid_multi.py`
+(multi-environment Gibson model) whose hot path runs on MI355X HIP kernels.
+
+Scripts bind the reference by module path (`from models import model_res_sigmoid_multi as
+md`, test/gib_plan.py:4, train/train_gib_multi.py:3); putting `p-ntfields_amd/` first on
+`sys.path` swaps this module in.  Class names, constructor signatures, method names,
+return shapes and state-dict keys are the reference's:
+
+    NN(device, dim)                              :131-175
+      .out(coords, B) -> (tau (N,1), coords)     :215-259   fused HIP forward (+ ∇τ if needed)
+      .out_grad(coords, B) -> (tau, dtau, coords):303-400   exact ∇τ (HIP reverse sweep)
+      .out_backgrad(coords, B) -> (...)          :402-647   HIP reverse sweep, quirk kept
+      .forward(coords, B)                        :850-854
+    Model(ModelPath, DataPath, dim, length, device)          :857-888
+      .gradient(y, x)  .Gradient(Xp, B)  .Speed/.Tau/.TravelTimes(Xp)  .load  .save
+
+Compute needs HIP device tensors; there is no CPU path (PntfError otherwise).  Training
+(`train`, `Loss`'s weight backward) and `plot` are outside this round's hot path and raise.
+"""
+import numpy as np
+import torch
+
+from pntf import ops
+from pntf.net import PackedCache, TauFunction, build_layers
+from pntf.net import init_weights as _init_weights
+
+
+# ---------------------------------------------------------------- activations (:76-127)
+def sigmoid(input):
+    return torch.sigmoid(10 * input)
+
+
+def sigmoid_out(input):
+    return torch.sigmoid(0.1 * input)
+
+
+class Sigmoid(torch.nn.Module):
+    def forward(self, input):
+        return sigmoid(input)
+
+
+class DSigmoid(torch.nn.Module):
+    def forward(self, input):
+        return 10 * sigmoid(input) * (1 - sigmoid(input))
+
+
+class Sigmoid_out(torch.nn.Module):
+    def forward(self, input):
+        return sigmoid_out(input)
+
+
+class DSigmoid_out(torch.nn.Module):
+    def forward(self, input):
+        return 0.1 * sigmoid_out(input) * (1 - sigmoid_out(input))
+
+
+class DDSigmoid_out(torch.nn.Module):
+    def forward(self, input):
+        s = sigmoid_out(input)
+        return 0.01 * s * (1 - s) * (1 - 2 * s)
+
+
+def _as_table(B, device):
+    """Reference B (dim,128) [or a per-env (E,dim,128) table] as a float32 device tensor."""
+    if not isinstance(B, torch.Tensor):
+        B = torch.as_tensor(np.asarray(B), dtype=torch.float32)
+    return B.to(device=device, dtype=torch.float32)
+
+
+class NN(torch.nn.Module):
+    """The sigmoid-residual MLP (model_res_sigmoid_multi.py:129-854)."""
+
+    def __init__(self, device, dim):
+        super().__init__()
+        self.dim = dim
+        self.input_size = 128
+        self.scale = 10
+        self.act = torch.nn.Softplus(beta=self.scale)
+        self.dact = Sigmoid()
+        self.ddact = DSigmoid()
+        self.actout = Sigmoid_out()
+        self.dactout = DSigmoid_out()
+        self.ddactout = DDSigmoid_out()
+        build_layers(self)
+        self._pack = PackedCache()
+
+    def init_weights(self, m):
+        _init_weights(m)
+
+    def packed(self):
+        return self._pack.get(self)
+
+    def input_mapping(self, x, B):
+        """Fourier features [sin 2πxB, cos 2πxB] (:186-190); a helper, not on the HIP path."""
+        w = 2.0 * np.pi * B
+        x_proj = x @ w
+        return torch.cat([torch.sin(x_proj), torch.cos(x_proj)], dim=-1)
+
+    def out(self, coords, B, env=None):
+        """τ (N,1) and the fresh grad-leaf coords (:215-259).  `env` (N,) int picks rows of a
+        per-env B table (E,dim,128); the reference passes a single (dim,128) B."""
+        coords = coords.clone().detach().requires_grad_(True)
+        tau = TauFunction.apply(coords, _as_table(B, coords.device), env, self.packed(),
+                                self.dim)
+        return tau, coords
+
+    def out_grad(self, coords, B, env=None):
+        """(τ (N,1), ∇τ (N,2dim), coords) — forward-mode Jacobian in the reference (:303-400);
+        the same values come from the exact HIP reverse sweep."""
+        t, d = ops.tau_grad(self.packed(), coords, _as_table(B, coords.device), env, self.dim,
+                            ops.GRAD_EXACT)
+        return t.unsqueeze(1), d, coords
+
+    def out_backgrad(self, coords, B, env=None):
+        """(τ, dτ, coords) of the reference's manual reverse mode (:402-647), including its
+        encoder[0] derivative quirk (:435-438) that test/gib_plan.py plans with."""
+        t, d = ops.tau_grad(self.packed(), coords, _as_table(B, coords.device), env, self.dim,
+                            ops.GRAD_BACKGRAD_COMPAT)
+        return t.unsqueeze(1), d, coords
+
+    def out_laplace(self, coords, B):
+        raise NotImplementedError(
+            "NN.out_laplace (Taylor-mode Eikonal residual, :710-848) is not on this round's "
+            "HIP path yet")
+
+    def forward(self, coords, B, env=None):
+        coords = coords.clone().detach().requires_grad_(True)
+        return self.out(coords, B, env)
+
+
+class Model:
+    """Model facade (model_res_sigmoid_multi.py:857-1293), inference part."""
+
+    def __init__(self, ModelPath, DataPath, dim, length, device="cpu"):
+        self.Params = {}
+        self.Params["ModelPath"] = ModelPath
+        self.Params["DataPath"] = DataPath
+        self.dim = dim
+        self.len = length
+        self.Params["Device"] = device
+        self.Params["Pytorch Amp (bool)"] = False
+        self.Params["Network"] = {"Normlisation": "OffsetMinMax"}
+        self.Params["Training"] = {
+            "Number of sample points": 2e5, "Batch Size": 2, "Validation Percentage": 10,
+            "Number of Epochs": 10000, "Resampling Bounds": [0.1, 0.9],
+            "Print Every * Epoch": 1, "Save Every * Epoch": 100, "Learning Rate": 1e-3,
+            "Random Distance Sampling": True, "Use Scheduler (bool)": False}
+        self.total_train_loss = []
+        self.total_val_loss = []
+
+    def gradient(self, y, x, create_graph=True):
+        """autograd ∇ (:890-896); through TauFunction it returns the HIP reverse sweep."""
+        grad_y = torch.ones_like(y)
+        return torch.autograd.grad(y, x, grad_y, only_inputs=True, retain_graph=True,
+                                   create_graph=create_graph)[0]
+
+    def Loss(self, points, Yobs, B, beta, gamma):
+        raise NotImplementedError("Model.Loss needs NN.out_laplace (Eikonal residual)")
+
+    def train(self):
+        raise NotImplementedError("training (Model.train, :953-1141) is outside the HIP hot "
+                                  "path of this round")
+
+    def save(self, epoch="", val_loss=""):
+        """Same checkpoint dict as the reference (:1143-1152)."""
+        opt = getattr(self, "optimizer", None)
+        torch.save({"epoch": epoch, "model_state_dict": self.network.state_dict(),
+                    "optimizer_state_dict": opt.state_dict() if opt is not None else {},
+                    "B_state_dict": getattr(self, "B", None),
+                    "train_loss": self.total_train_loss, "val_loss": self.total_val_loss},
+                   "{}/Model_Epoch_{}_ValLoss_{:.6e}.pt".format(
+                       self.Params["ModelPath"], str(epoch).zfill(5), val_loss))
+
+    def load(self, filepath):
+        """Weights only, like the reference (:1154-1166; B is not restored, :1159)."""
+        checkpoint = torch.load(filepath, map_location=torch.device(self.Params["Device"]),
+                                weights_only=True)
+        self.network = NN(self.Params["Device"], self.dim)
+        self.network.load_state_dict(checkpoint["model_state_dict"], strict=True)
+        self.network.to(torch.device(self.Params["Device"]))
+        self.network.float()
+        self.network.eval()
+
+    def _dev(self):
+        return torch.device(self.Params["Device"])
+
+    def TravelTimes(self, Xp):
+        """|x_g - x_s| / τ (:1173-1186), uses self.B."""
+        Xp = Xp.to(self._dev())
+        return ops.travel_time(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                               self.dim)
+
+    def Tau(self, Xp):
+        """τ (N,1) (:1188-1193), uses self.B."""
+        Xp = Xp.to(self._dev())
+        return ops.tau(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                       self.dim).unsqueeze(1)
+
+    def Speed(self, Xp):
+        """Speed at the goal (:1195-1216), uses self.B."""
+        Xp = Xp.to(self._dev())
+        return ops.speed(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                         self.dim)
+
+    def Gradient(self, Xp, B, env=None):
+        """Path velocity [v_s | v_g] (:1218-1248) from the out_backgrad sweep (quirk kept),
+        per-row norms."""
+        Xp = Xp.to(self._dev())
+        v, _ = ops.path_velocity(self.network.packed(), Xp, _as_table(B, Xp.device), env,
+                                 self.dim, ops.GRAD_BACKGRAD_COMPAT)
+        return v
+
+    def Plan(self, XP, B, step=0.03, tol=0.06, max_iter=500, env=None,
+             mode=ops.GRAD_BACKGRAD_COMPAT):
+        """Batched test/gib_plan.py:74-86 loop on device: Q independent queries, each frozen
+        once |x_g - x_s| <= tol.  Returns (path (Q, max_iter+2, 2dim), steps (Q,))."""
+        XP = XP.to(self._dev())
+        return ops.plan(self.network.packed(), XP, _as_table(B, XP.device), env, self.dim,
+                        step, tol, max_iter, mode)
+
+    def plot(self, epoch, total_train_loss, alpha):
+        raise NotImplementedError("Model.plot (matplotlib field plots) is not on the hot path")

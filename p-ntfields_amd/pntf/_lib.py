@@ -1,0 +1,79 @@
+"""ctypes binding of libpntf.so (C ABI declared in include/pntf.h).
+
+The library is built in-tree by `__graft_entry__.build()` (hipcc, gfx950) and loaded from
+this directory.  There is no fallback: if the library is missing every compute entry point
+raises, so a GPU run can never silently take a CPU path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpntf.so")
+
+GRAD_EXACT = 0
+GRAD_BACKGRAD_COMPAT = 1
+
+_c_void_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_size = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/pntf.h exactly
+SIGNATURES = {
+    "pntf_abi_version": (ctypes.c_int, []),
+    "pntf_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "pntf_last_error": (ctypes.c_char_p, []),
+    "pntf_packed_floats": (_size, []),
+    "pntf_pack_weights": (ctypes.c_int, [ctypes.POINTER(_c_void_p), ctypes.c_int, _c_void_p,
+                                         _c_void_p]),
+    "pntf_workspace_bytes": (_size, [_i64]),
+    "pntf_tau": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                _i32, _c_void_p, _c_void_p]),
+    "pntf_tau_grad": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
+                                     _c_void_p, _i32, ctypes.c_int, _c_void_p, _c_void_p,
+                                     _c_void_p, _size, _c_void_p]),
+    "pntf_path_velocity": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
+                                          _c_void_p, _i32, ctypes.c_int, _c_void_p, _c_void_p,
+                                          _c_void_p, _size, _c_void_p]),
+    "pntf_speed": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
+                                  _c_void_p, _i32, _c_void_p, _c_void_p, _size, _c_void_p]),
+    "pntf_travel_time": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
+                                        _c_void_p, _i32, _c_void_p, _c_void_p]),
+    "pntf_plan": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
+                                 _c_void_p, _i32, ctypes.c_int, _f32, _f32, _i32, _c_void_p,
+                                 _c_void_p, _c_void_p, _size, _c_void_p]),
+}
+
+_lib = None
+
+
+class PntfError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libpntf.so once; raise (never fall back) if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PntfError(
+            "libpntf.so not found at %s — build it with `python -c 'import __graft_entry__ as g;"
+            " g.build()'` (hipcc --offload-arch=gfx950)" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.pntf_abi_version() != 1:
+        raise PntfError("libpntf ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(status, what):
+    if status != 0:
+        lib = load()
+        raise PntfError("%s failed: %s (%s)" % (
+            what, lib.pntf_status_string(status).decode(), lib.pntf_last_error().decode()))

@@ -1,0 +1,172 @@
+"""Torch-facing wrappers of the libpntf C ABI (device tensors in, device tensors out).
+
+Every call is stream-ordered on torch's current HIP stream of the input's device; torch's
+caching allocator owns all buffers (outputs and the scratch workspace).  Inputs must be
+HIP (``cuda``) tensors: there is deliberately no CPU path.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import GRAD_BACKGRAD_COMPAT, GRAD_EXACT, PntfError, check
+
+__all__ = ["GRAD_EXACT", "GRAD_BACKGRAD_COMPAT", "PntfError", "pack_weights", "tau",
+           "tau_grad", "path_velocity", "speed", "travel_time", "plan", "packed_floats",
+           "workspace_bytes"]
+
+_ws_cache = {}
+
+
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_device(t, name):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise PntfError("%s must be a HIP device tensor (got %s); the P-NTFields MI355X path "
+                        "has no CPU fallback" % (name, getattr(t, "device", type(t))))
+
+
+def packed_floats():
+    return int(_lib.load().pntf_packed_floats())
+
+
+def workspace_bytes(n):
+    return int(_lib.load().pntf_workspace_bytes(int(n)))
+
+
+def _workspace(device, n):
+    """Grow-only scratch buffer per device (saved σ10 tiles of the reverse sweep)."""
+    need = workspace_bytes(n)
+    key = (device.type, device.index)
+    ws = _ws_cache.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=device)
+        _ws_cache[key] = ws
+    return ws
+
+
+def pack_weights(params, out=None):
+    """Pack the 30 state-dict tensors (reference order, see synth.state_dict_keys) into the
+    MFMA fragment blob consumed by every kernel (pntf_pack_weights)."""
+    lib = _lib.load()
+    params = list(params)
+    if len(params) != 30:
+        raise PntfError("expected the 30 state-dict tensors of NN, got %d" % len(params))
+    dev = params[0].device
+    ts = []
+    for i, p in enumerate(params):
+        _require_device(p, "param[%d]" % i)
+        ts.append(p.detach().to(torch.float32).contiguous())
+    if out is None:
+        out = torch.empty(packed_floats(), dtype=torch.float32, device=dev)
+    arr = (ctypes.c_void_p * 30)(*[t.data_ptr() for t in ts])
+    check(lib.pntf_pack_weights(arr, 30, _vp(out), _stream(dev)), "pntf_pack_weights")
+    return out
+
+
+def _prep(xp, Btab, env, dim):
+    _require_device(xp, "xp")
+    if dim not in (3, 6):
+        raise PntfError("dim must be 3 or 6")
+    if xp.dim() != 2 or xp.shape[1] != 2 * dim:
+        raise PntfError("xp must be (n, %d), got %s" % (2 * dim, tuple(xp.shape)))
+    xp = xp.detach().to(torch.float32).contiguous()
+    _require_device(Btab, "B")
+    Bt = Btab.detach().to(device=xp.device, dtype=torch.float32)
+    if Bt.dim() == 2:
+        Bt = Bt.unsqueeze(0)
+    if Bt.dim() != 3 or Bt.shape[1] != dim or Bt.shape[2] != 128:
+        raise PntfError("B must be (dim, 128) or (n_env, dim, 128), got %s" % (tuple(Btab.shape),))
+    Bt = Bt.contiguous()
+    if env is not None:
+        _require_device(env, "env")
+        if env.numel() != xp.shape[0]:
+            raise PntfError("env must hold one id per pair")
+        env = env.detach().to(torch.int32).contiguous()
+    return xp, Bt, env
+
+
+def tau(packed, xp, Btab, env=None, dim=3):
+    """τ (n,) — NN.out (model_res_sigmoid_multi.py:215-259)."""
+    lib = _lib.load()
+    xp, Bt, env = _prep(xp, Btab, env, dim)
+    n = xp.shape[0]
+    out = torch.empty(n, dtype=torch.float32, device=xp.device)
+    check(lib.pntf_tau(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0], _vp(out),
+                       _stream(xp.device)), "pntf_tau")
+    return out
+
+
+def tau_grad(packed, xp, Btab, env=None, dim=3, mode=GRAD_EXACT):
+    """τ (n,) and ∇τ (n, 2dim): Model.gradient(NN.out) (EXACT) or NN.out_backgrad (COMPAT)."""
+    lib = _lib.load()
+    xp, Bt, env = _prep(xp, Btab, env, dim)
+    n = xp.shape[0]
+    t = torch.empty(n, dtype=torch.float32, device=xp.device)
+    d = torch.empty((n, 2 * dim), dtype=torch.float32, device=xp.device)
+    ws = _workspace(xp.device, n)
+    check(lib.pntf_tau_grad(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0], mode,
+                            _vp(t), _vp(d), _vp(ws), ws.numel(), _stream(xp.device)),
+          "pntf_tau_grad")
+    return t, d
+
+
+def path_velocity(packed, xp, Btab, env=None, dim=3, mode=GRAD_BACKGRAD_COMPAT):
+    """[v_start | v_goal] (n, 2dim) and τ (n,) — Model.Gradient (:1218-1248)."""
+    lib = _lib.load()
+    xp, Bt, env = _prep(xp, Btab, env, dim)
+    n = xp.shape[0]
+    v = torch.empty((n, 2 * dim), dtype=torch.float32, device=xp.device)
+    t = torch.empty(n, dtype=torch.float32, device=xp.device)
+    ws = _workspace(xp.device, n)
+    check(lib.pntf_path_velocity(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0],
+                                 mode, _vp(v), _vp(t), _vp(ws), ws.numel(), _stream(xp.device)),
+          "pntf_path_velocity")
+    return v, t
+
+
+def speed(packed, xp, Btab, env=None, dim=3):
+    """Speed at the goal (n,) — Model.Speed (:1195-1216)."""
+    lib = _lib.load()
+    xp, Bt, env = _prep(xp, Btab, env, dim)
+    n = xp.shape[0]
+    s = torch.empty(n, dtype=torch.float32, device=xp.device)
+    ws = _workspace(xp.device, n)
+    check(lib.pntf_speed(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0], _vp(s),
+                         _vp(ws), ws.numel(), _stream(xp.device)), "pntf_speed")
+    return s
+
+
+def travel_time(packed, xp, Btab, env=None, dim=3):
+    """|x_g - x_s| / τ (n,) — Model.TravelTimes (:1173-1186)."""
+    lib = _lib.load()
+    xp, Bt, env = _prep(xp, Btab, env, dim)
+    n = xp.shape[0]
+    tt = torch.empty(n, dtype=torch.float32, device=xp.device)
+    check(lib.pntf_travel_time(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0],
+                               _vp(tt), _stream(xp.device)), "pntf_travel_time")
+    return tt
+
+
+def plan(packed, xp0, Btab, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
+         mode=GRAD_BACKGRAD_COMPAT):
+    """Batched bidirectional planner (test/gib_plan.py:74-86; arm: test/arm_plan.py:140-152).
+
+    Returns path (q, max_iter + 2, 2dim) — row 0 the start, frozen rows repeating the final
+    state — and steps (q,) int32 (updates taken per query)."""
+    lib = _lib.load()
+    xp0, Bt, env = _prep(xp0, Btab, env, dim)
+    q = xp0.shape[0]
+    path = torch.empty((q, max_iter + 2, 2 * dim), dtype=torch.float32, device=xp0.device)
+    steps = torch.empty(q, dtype=torch.int32, device=xp0.device)
+    ws = _workspace(xp0.device, q)
+    check(lib.pntf_plan(_vp(packed), dim, _vp(xp0), q, _vp(Bt), _vp(env), Bt.shape[0], mode,
+                        float(step), float(tol), int(max_iter), _vp(path), _vp(steps), _vp(ws),
+                        ws.numel(), _stream(xp0.device)), "pntf_plan")
+    return path, steps

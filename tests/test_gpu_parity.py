@@ -1,0 +1,234 @@
+"""HIP path (libpntf.so through the C ABI / drop-in models) vs the reference goldens and
+the CPU oracle.
+
+Tolerance (BASELINE.json north_star): τ and ∇τ within 1e-4 relative (fp32) of the
+reference — checked as relative L2 over the batch AND as the max abs error over the max
+|value|; planner endpoints within 1e-3 of the reference's batch-1 loop.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import load, rel_l2, weights
+from oracle import pntf_oracle as O
+from pntf import ops, synth
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-4
+
+
+def close(a, b, tol=REL):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    l2 = rel_l2(a, b)
+    mx = float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+    assert l2 < tol and mx < tol, "rel_l2=%.3g max=%.3g (tol %.1g)" % (l2, mx, tol)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def W():
+    return weights()
+
+
+@pytest.fixture(scope="module")
+def packed(W, dev):
+    params = [torch.from_numpy(v).to(dev) for v in W.values()]
+    return ops.pack_weights(params)
+
+
+def T(a, dev, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device=dev, dtype=dtype)
+
+
+def test_tau_grad_exact_vs_reference(packed, dev):
+    f = load("fwd_grad_d3.npz")
+    t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3, mode=ops.GRAD_EXACT)
+    close(t.cpu().numpy(), f["tau"][:, 0])
+    close(d.cpu().numpy(), f["dtau"])
+    close(d.cpu().numpy(), f["dtau_fwdmode"])
+
+
+def test_tau_only_kernel(packed, dev):
+    f = load("fwd_grad_d3.npz")
+    t = ops.tau(packed, T(f["xp"], dev), T(f["B"], dev), dim=3)
+    close(t.cpu().numpy(), f["tau"][:, 0])
+
+
+def test_backgrad_compat_vs_reference(packed, dev):
+    f = load("fwd_grad_d3.npz")
+    t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3,
+                        mode=ops.GRAD_BACKGRAD_COMPAT)
+    close(t.cpu().numpy(), f["tau_backgrad"][:, 0])
+    close(d.cpu().numpy(), f["dtau_backgrad"])
+
+
+def test_epilogues_vs_reference(packed, dev):
+    f = load("fwd_grad_d3.npz")
+    xp, B = T(f["xp"], dev), T(f["B"], dev)
+    v, _ = ops.path_velocity(packed, xp, B, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT)
+    close(v.cpu().numpy(), f["gradient"])
+    close(ops.speed(packed, xp, B, dim=3).cpu().numpy(), f["speed"])
+    close(ops.travel_time(packed, xp, B, dim=3).cpu().numpy(), f["travel_time"])
+
+
+def test_env_table_vs_reference(packed, dev):
+    g = load("fwd_grad_env_d3.npz")
+    xp, Bt, env = T(g["xp"], dev), T(g["B_table"], dev), T(g["env"], dev, torch.int32)
+    t, d = ops.tau_grad(packed, xp, Bt, env, dim=3)
+    close(t.cpu().numpy(), g["tau"][:, 0])
+    close(d.cpu().numpy(), g["dtau"])
+    _, dc = ops.tau_grad(packed, xp, Bt, env, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT)
+    close(dc.cpu().numpy(), g["dtau_backgrad"])
+
+
+def test_arm_dim6_vs_reference(packed, dev):
+    a = load("fwd_grad_d6.npz")
+    xp, B = T(a["xp"], dev), T(a["B"].T, dev)
+    t, d = ops.tau_grad(packed, xp, B, dim=6)
+    close(t.cpu().numpy(), a["tau"][:, 0])
+    close(d.cpu().numpy(), a["dtau"])
+    v, _ = ops.path_velocity(packed, xp[:16], B, dim=6, mode=ops.GRAD_EXACT)
+    close(v.cpu().numpy(), a["gradient16"])
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 33, 1000, 4099])
+def test_ragged_batches_vs_oracle(packed, dev, W, n):
+    xp = synth.make_pairs(n, 3, seed=100 + n)
+    Bt = synth.make_B_table(3, 3, first_seed=20)
+    env = synth.make_env_ids(n, 3, contiguous=False, seed=n)
+    t, d = ops.tau_grad(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3)
+    to, do = O.tau_grad(W, xp, Bt, env)
+    close(t.cpu().numpy(), to[:, 0])
+    close(d.cpu().numpy(), do)
+
+
+def test_empty_batch(packed, dev):
+    xp = torch.zeros((0, 6), device=dev)
+    t, d = ops.tau_grad(packed, xp, T(synth.make_B(3), dev), dim=3)
+    assert t.shape == (0,) and d.shape == (0, 6)
+
+
+def test_invalid_env_gives_nan(packed, dev):
+    xp = synth.make_pairs(20, 3, seed=5)
+    Bt = synth.make_B_table(2, 3)
+    env = np.zeros(20, np.int32)
+    env[3] = 7
+    env[11] = -1
+    t, d = ops.tau_grad(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3)
+    t, d = t.cpu().numpy(), d.cpu().numpy()
+    assert np.isnan(t[3]) and np.isnan(t[11]) and np.isnan(d[3]).all()
+    ok = np.ones(20, bool)
+    ok[[3, 11]] = False
+    assert np.isfinite(t[ok]).all() and np.isfinite(d[ok]).all()
+
+
+def test_coincident_endpoints(packed, dev, W):
+    """xs == xg: τ and ∇τ are finite (the merge is symmetric), Speed = τ."""
+    x = synth.make_pairs(8, 3, seed=9)
+    x[:, 3:] = x[:, :3]
+    B = synth.make_B(3)
+    t, d = ops.tau_grad(packed, T(x, dev), T(B, dev), dim=3)
+    to, do = O.tau_grad(W, x, B)
+    close(t.cpu().numpy(), to[:, 0])
+    close(d.cpu().numpy(), do)
+
+
+def test_gibson_planner_vs_reference(packed, dev):
+    p = load("plan_gib.npz")
+    path, steps = ops.plan(packed, T(p["starts"], dev), T(p["B"], dev), dim=3, step=0.03,
+                           tol=0.06, max_iter=500, mode=ops.GRAD_BACKGRAD_COMPAT)
+    path, steps = path.cpu().numpy(), steps.cpu().numpy()
+    np.testing.assert_array_equal(steps, p["iters"])
+    assert np.abs(path - p["paths"]).max() < 1e-3
+    # endpoints
+    last = p["paths"][np.arange(len(steps)), steps]
+    assert np.abs(path[np.arange(len(steps)), steps] - last).max() < 1e-3
+
+
+def test_arm_planner_vs_reference(packed, dev):
+    p = load("plan_arm.npz")
+    path, steps = ops.plan(packed, T(p["starts"], dev), T(p["B"].T, dev), dim=6, step=0.015,
+                           tol=0.03, max_iter=300, mode=ops.GRAD_EXACT)
+    path, steps = path.cpu().numpy(), steps.cpu().numpy()
+    np.testing.assert_array_equal(steps, p["iters"])
+    assert np.abs(path - p["paths"]).max() < 1e-3
+
+
+def test_planner_batch_vs_oracle(packed, dev, W):
+    q = 37
+    xp0 = synth.make_box_pairs(q, 6, seed=77)
+    B = synth.make_B(6, seed=12, arm=True).T.copy()
+    path, steps = ops.plan(packed, T(xp0, dev), T(B, dev), dim=6, step=0.015, tol=0.03,
+                           max_iter=60, mode=ops.GRAD_EXACT)
+    po, so = O.plan(W, xp0, B, dim=6, step=0.015, tol=0.03, max_iter=60, compat=False)
+    np.testing.assert_array_equal(steps.cpu().numpy(), so)
+    assert np.abs(path.cpu().numpy() - po).max() < 1e-3
+
+
+def test_drop_in_models_api(W, dev):
+    """The reference call sequence of test/gib_plan.py / Model.gradient through the
+    drop-in modules."""
+    from models import model_res_sigmoid_multi as md
+    f = load("fwd_grad_d3.npz")
+    m = md.Model(".", ".", 3, 2, device="cuda")
+    m.network = md.NN("cuda", 3)
+    m.network.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m.network.to(dev).float().eval()
+    xp, B = T(f["xp"], dev), T(f["B"], dev)
+    tau, coords = m.network.out(xp, B)
+    assert tau.shape == (1024, 1)
+    dtau = m.gradient(tau, coords)
+    close(tau.detach().cpu().numpy(), f["tau"])
+    close(dtau.cpu().numpy(), f["dtau"])
+    close(m.Gradient(xp.clone(), B).cpu().numpy(), f["gradient"])
+    m.B = B
+    close(m.Speed(xp).cpu().numpy(), f["speed"])
+    close(m.TravelTimes(xp).cpu().numpy(), f["travel_time"])
+    close(m.Tau(xp).cpu().numpy(), f["tau"])
+    t2, d2, _ = m.network.out_backgrad(xp, B)
+    close(d2.cpu().numpy(), f["dtau_backgrad"])
+    # weights edited in place -> repacked
+    with torch.no_grad():
+        m.network.generator[4].bias.add_(0.5)
+    t3, _ = m.network.out(xp, B)
+    assert not torch.allclose(t3, tau)
+
+
+def test_arm_models_api(W, dev):
+    from models import model_res_sigmoid as ma
+    a = load("fwd_grad_d6.npz")
+    m = ma.Model(".", ".", 6, device="cuda")
+    m.B = torch.from_numpy(a["B"])
+    m.network = ma.NN("cuda", 6, m.B)
+    m.network.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m.network.to(dev)
+    xp = T(a["xp"], dev)
+    tau, coords = m.network.out(xp)
+    close(m.gradient(tau, coords).cpu().numpy(), a["dtau"])
+    g = torch.cat([m.Gradient(xp[i:i + 1].clone()) for i in range(16)])
+    close(g.cpu().numpy(), a["gradient16"])
+
+
+def test_large_batch_properties(packed, dev):
+    """Full-size (C2: 262 144 pairs) properties: finite, τ in (0,1), tile-boundary-free
+    (a permuted batch gives the permuted answer), a sampled subset matches the oracle."""
+    n = 262144
+    xp = synth.make_pairs(n, 3, seed=2)
+    B = synth.make_B(3, seed=1)
+    t, d = ops.tau_grad(packed, T(xp, dev), T(B, dev), dim=3)
+    t, d = t.cpu().numpy(), d.cpu().numpy()
+    assert np.isfinite(t).all() and np.isfinite(d).all() and (t > 0).all() and (t < 1).all()
+    perm = np.random.default_rng(0).permutation(n)
+    tp, dp = ops.tau_grad(packed, T(xp[perm], dev), T(B, dev), dim=3)
+    np.testing.assert_array_equal(tp.cpu().numpy(), t[perm])
+    np.testing.assert_array_equal(dp.cpu().numpy(), d[perm])
+    idx = np.random.default_rng(1).choice(n, 512, replace=False)
+    to, do = O.tau_grad(weights(), xp[idx], B)
+    close(t[idx], to[:, 0])
+    close(d[idx], do)

@@ -1,0 +1,138 @@
+"""CPU-only checks of the boundary: libpntf.so loads and exports exactly the C ABI of
+include/pntf.h; host logic (state-dict layout, packing layout, argument validation, no
+CPU fallback) behaves like the reference interface."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from pntf import _lib, ops, synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pntf.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(pntf_\w+)\s*\(", txt, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        from pntf import build
+        build.build()
+    return ctypes.CDLL(_lib.LIB_PATH)
+
+
+def test_header_declares_expected_entry_points():
+    syms = header_symbols()
+    for s in ("pntf_pack_weights", "pntf_tau", "pntf_tau_grad", "pntf_path_velocity",
+              "pntf_speed", "pntf_travel_time", "pntf_plan", "pntf_workspace_bytes"):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol(lib):
+    for s in header_symbols():
+        assert hasattr(lib, s), s
+    assert set(header_symbols()) == set(_lib.SIGNATURES)
+
+
+def test_pure_queries_without_gpu(lib):
+    lib.pntf_abi_version.restype = ctypes.c_int
+    assert lib.pntf_abi_version() == 1
+    lib.pntf_packed_floats.restype = ctypes.c_size_t
+    # forward + transposed fragments of 13 matrices + biases/head
+    mats = 128 * 256 + 4 * 128 * 128 + 128 * 128 + 6 * 256 * 256 + 128 * 256
+    assert lib.pntf_packed_floats() == 2 * mats + 128 + 4 * 128 + 128 + 6 * 256 + 128 + 128 + 4
+    lib.pntf_status_string.restype = ctypes.c_char_p
+    assert lib.pntf_status_string(1) == b"invalid argument"
+
+
+def test_argument_validation_without_gpu(lib):
+    L = _lib.load()
+    # dim must be 3 or 6; checked before any device access
+    st = L.pntf_tau(None, 4, None, 10, None, None, 1, None, None)
+    assert st == 1 and b"dim" in L.pntf_last_error()
+    # empty batch is a no-op whatever the pointers are
+    assert L.pntf_tau_grad(None, 3, None, 0, None, None, 1, 0, None, None, None, 0, None) == 0
+    assert L.pntf_plan(None, 6, None, 0, None, None, 1, 0, 0.1, 0.1, 5, None, None, None, 0,
+                       None) == 0
+    assert L.pntf_plan(None, 6, None, 4, None, None, 1, 0, 0.1, 0.1, -1, None, None, None, 0,
+                       None) == 1
+
+
+def test_no_cpu_fallback():
+    W = synth.make_weights(0)
+    with pytest.raises(_lib.PntfError, match="HIP device"):
+        ops.pack_weights([torch.from_numpy(v) for v in W.values()])
+    with pytest.raises(_lib.PntfError, match="HIP device"):
+        ops.tau(None, torch.zeros(4, 6), torch.zeros(3, 128))
+
+
+def test_drop_in_state_dict_matches_reference_layout():
+    from models import model_res_sigmoid as ma
+    from models import model_res_sigmoid_multi as md
+    net = md.NN("cpu", 3)
+    assert list(net.state_dict().keys()) == synth.state_dict_keys()
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    for name, fo, fi in synth.LAYER_SHAPES:
+        assert shapes[name + ".weight"] == (fo, fi) and shapes[name + ".bias"] == (fo,)
+    W = synth.make_weights(0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    arm = ma.NN("cpu", 6, torch.zeros(128, 6))
+    assert list(arm.state_dict().keys()) == synth.state_dict_keys()
+    assert tuple(arm.B.shape) == (6, 128)
+    net.apply(net.init_weights)   # reference init U(±2/sqrt(fan_in))
+    w = net.generator[0].weight.detach().numpy()
+    assert np.abs(w).max() <= 2 / np.sqrt(256) + 1e-7
+
+
+def test_models_raise_on_cpu_compute():
+    from models import model_res_sigmoid_multi as md
+    m = md.Model(".", ".", 3, 2, device="cpu")
+    m.network = md.NN("cpu", 3)
+    with pytest.raises(_lib.PntfError):
+        m.network.out(torch.zeros(4, 6), torch.zeros(3, 128))
+    with pytest.raises(NotImplementedError):
+        m.train()
+
+
+def _pack_index_numpy(W, trans):
+    """numpy restatement of pack_kernel's index map (pntf_field.h)."""
+    M = W.T if trans else W
+    rows, cols = M.shape
+    o = np.arange(rows * cols)
+    s, lane, rest = o & 3, (o >> 2) & 63, o >> 8
+    KT = cols // 16
+    kt, ot = rest % KT, rest // KT
+    n = 16 * ot + (lane & 15)
+    k = 16 * kt + 4 * (lane >> 4) + s
+    return M[n, k]
+
+
+def test_pack_layout_is_a_permutation_and_feeds_mfma_fragments():
+    rng = np.random.default_rng(0)
+    W = rng.standard_normal((128, 256)).astype(np.float32)
+    P = _pack_index_numpy(W, False)
+    assert np.array_equal(np.sort(P), np.sort(W.ravel()))
+    # fragment (ot, kt), lane (i, g), s  ==  W[16 ot + i][16 kt + 4 g + s]
+    frag = P.reshape(8, 16, 64, 4)
+    ot, kt, i, g = 3, 11, 5, 2
+    np.testing.assert_array_equal(frag[ot, kt, g * 16 + i], W[16 * ot + i, 16 * kt + 4 * g:16 * kt + 4 * g + 4])
+    PT = _pack_index_numpy(W, True)
+    fragT = PT.reshape(16, 8, 64, 4)
+    ot, kt = 13, 6
+    np.testing.assert_array_equal(fragT[ot, kt, g * 16 + i],
+                                  W.T[16 * ot + i, 16 * kt + 4 * g:16 * kt + 4 * g + 4])
+
+
+def test_synth_is_deterministic():
+    np.testing.assert_array_equal(synth.make_pairs(100, 3, 2), synth.make_pairs(100, 3, 2))
+    x = synth.make_pairs(5000, 3, 2)
+    assert x.shape == (5000, 6) and np.all(np.abs(x) <= 0.5)
+    e = synth.make_env_ids(1048576, 10)
+    assert e.min() == 0 and e.max() == 9 and np.all(np.diff(e) >= 0)

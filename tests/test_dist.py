@@ -1,0 +1,64 @@
+"""Multi-process sharding path on CPU (gloo, world_size 2): each rank evaluates its
+contiguous shard (here with the oracle standing in for the HIP kernel, which needs a GPU)
+and the RCCL/gloo all-gather of per-rank rows reassembles the full batch in order."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from pntf import dist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as tdist
+    from oracle import pntf_oracle as O
+    from pntf import synth
+    r, ws = dist.init("gloo")
+    assert (r, ws) == (rank, world)
+    W = synth.make_weights(0)
+    xp = synth.make_pairs(n, 3, seed=2)
+    B = synth.make_B(3)
+    lo, hi = dist.shard_range(n, rank, world)
+    t, d = O.tau_grad(W, xp[lo:hi], B, dtype=np.float32)
+    local = torch.from_numpy(np.concatenate([t, d], 1).astype(np.float32))
+    full = dist.all_gather_rows(local, n)
+    tf, df = O.tau_grad(W, xp, B, dtype=np.float32)
+    np.testing.assert_allclose(full.numpy(), np.concatenate([tf, df], 1), rtol=1e-5, atol=1e-6)
+    # planner paths gathered the same way (q queries, uneven shards)
+    xq = synth.make_pairs(q, 3, seed=11)
+    lo, hi = dist.shard_range(q, rank, world)
+    p, s = O.plan(W, xq[lo:hi], B, max_iter=20, dtype=np.float32)
+    paths = dist.all_gather_rows(torch.from_numpy(p.astype(np.float32)), q)
+    pf, sf = O.plan(W, xq, B, max_iter=20, dtype=np.float32)
+    np.testing.assert_allclose(paths.numpy(), pf, rtol=1e-5, atol=1e-6)
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 1000, 1048577):
+        for w in (1, 2, 3, 8):
+            ranges = [dist.shard_range(n, r, w) for r in range(w)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+            sizes = [h - l for l, h in ranges]
+            assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("n,q", [(100, 5), (64, 4)])
+def test_gloo_world2_gather(n, q):
+    port = _free_port()
+    mp.start_processes(_worker, args=(2, port, n, q), nprocs=2, join=True, start_method="spawn")

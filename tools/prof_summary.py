@@ -1,0 +1,77 @@
+"""Summarise rocprofv3 outputs (gpurun_out/) into committed profiles/ files.
+
+    python tools/prof_summary.py --tag r01 --pairs 1048576 [--kernel field_kernel<3, 1>]
+
+Reads gpurun_out/prof_stats/run_kernel_stats.csv (kernel-trace --stats) and the separate
+PMC passes gpurun_out/pmc_{fetch,write,mfma}/run_counter_collection.csv, applies the gfx950
+corrections of MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of 16-B/lane streaming
+reads: doubled; WRITE_SIZE exact for 16-B/lane stores; both in KiB), and writes
+profiles/<tag>_kernel_stats.csv and profiles/<tag>_pmc_tau_grad.json; the latter is also
+copied to profiles/pmc_tau_grad.json, which bench.py reads for roofline.traffic.
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+
+
+def counters(run, kernel):
+    path = os.path.join(OUT, run, "run_counter_collection.csv")
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default="r01")
+    ap.add_argument("--pairs", type=int, default=1 << 20)
+    ap.add_argument("--kernel", default="field_kernel<3, 1>")
+    a = ap.parse_args()
+    os.makedirs(PROF, exist_ok=True)
+    stats = os.path.join(OUT, "prof_stats", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(PROF, "%s_kernel_stats.csv" % a.tag))
+    avg_ns = None
+    for r in csv.DictReader(open(stats)):
+        if a.kernel in r["Name"]:
+            avg_ns = float(r["AverageNs"])
+    fetch, nf = counters("pmc_fetch", a.kernel)
+    write, nw = counters("pmc_write", a.kernel)
+    mfma, nm = counters("pmc_mfma", a.kernel)
+    fetch_b = fetch["FETCH_SIZE"] * 1024 * 2
+    write_b = write["WRITE_SIZE"] * 1024
+    flops = mfma["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512
+    clock = mfma["GRBM_GUI_ACTIVE"] / 8 / (avg_ns * 1e-9) / 1e9
+    simd_cycles = 1024 * avg_ns * 1e-9 * clock * 1e9
+    j = {
+        "kernel": a.kernel, "pairs_per_launch": a.pairs, "avg_duration_ns": avg_ns,
+        "FETCH_SIZE_KiB": fetch["FETCH_SIZE"], "WRITE_SIZE_KiB": write["WRITE_SIZE"],
+        "fetch_bytes_corrected_x2": fetch_b, "write_bytes": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "hbm_bytes_per_pair": (fetch_b + write_b) / a.pairs,
+        "hbm_GBps": (fetch_b + write_b) / (avg_ns * 1e-9) / 1e9,
+        "mfma_flops_per_launch": flops, "mfma_flops_per_pair": flops / a.pairs,
+        "mfma_busy_cycles": mfma["SQ_VALU_MFMA_BUSY_CYCLES"],
+        "mfma_busy_frac_of_simd_cycles": mfma["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles,
+        "effective_clock_GHz": clock, "sq_waves": mfma.get("SQ_WAVES"),
+        "dispatches_averaged": {"fetch": nf, "write": nw, "mfma": nm},
+        "notes": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 counts half of 16-B/lane "
+                 "streaming reads); Infinity-Cache hits are counted as fetches.",
+    }
+    p = os.path.join(PROF, "%s_pmc_tau_grad.json" % a.tag)
+    with open(p, "w") as fh:
+        json.dump(j, fh, indent=1)
+    shutil.copy(p, os.path.join(PROF, "pmc_tau_grad.json"))
+    print(json.dumps(j, indent=1))
+
+
+if __name__ == "__main__":
+    main()

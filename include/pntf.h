@@ -99,6 +99,19 @@ int pntf_plan(const float* packed, int dim, const float* xp0, int64_t q, const f
               int32_t max_iter, float* path, int32_t* steps, void* ws, size_t ws_bytes,
               hipStream_t stream);
 
+/* Eikonal residual: NN.out_laplace + the per-pair residual of Model.Loss
+ * (model_res_sigmoid_multi.py:710-848, :897-946), Taylor mode.  Each output may be NULL:
+ * tau (n), dtau (n, 2*dim), ltau (n, 2*dim) diagonal second derivatives, diff (n) the
+ * residual loss0 + loss1 - 4 for observed speeds yobs (n, 2) (required when diff != NULL)
+ * and viscosity weight gamma (0.001 in the reference training, :1015). */
+int pntf_eikonal_residual(const float* packed, int dim, const float* xp, const float* yobs,
+                          int64_t n, const float* Btab, const int32_t* env, int32_t n_env,
+                          float gamma, float* tau, float* dtau, float* ltau, float* diff,
+                          void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* Deterministic fp64 sum of x (n) into *out (device pointer to one double). */
+int pntf_sum(const float* x, int64_t n, double* out, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

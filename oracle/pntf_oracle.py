@@ -319,6 +319,27 @@ def eikonal_residual(params, xp, yobs, B, env=None, dim=3, gamma=1e-3, dtype=np.
     return tau, dtau, ltau, diff
 
 
+def eikonal_residual_arm(params, xp, yobs, B, dim=6, gamma=1e-3, dtype=np.float64):
+    """The arm model's residual (models/model_res_sigmoid.py:869-935): square-root speeds
+    and viscosity applied to 1/Ypred; B is the (dim, 128) = B_state_dict.T table."""
+    tau, dtau, ltau = laplace(params, xp, B, None, dim, dtype)
+    xp = np.asarray(xp, dtype=dtype)
+    yobs = np.asarray(yobs, dtype=dtype)
+    D = xp[:, dim:] - xp[:, :dim]
+    T0 = np.sum(D * D, axis=1)
+    lap0, lap1 = ltau[:, :dim].sum(-1), ltau[:, dim:].sum(-1)
+    DT0, DT1 = dtau[:, :dim], dtau[:, dim:]
+    t = tau[:, 0]
+    T3 = t * t
+    S0 = T0 * np.sum(DT0 * DT0, 1) + 2 * t * np.sum(DT0 * D, 1) + T3
+    S1 = T0 * np.sum(DT1 * DT1, 1) - 2 * t * np.sum(DT1 * D, 1) + T3
+    yp0 = np.sqrt(1.0 / (1.0 / (T3 / np.sqrt(S0)) + gamma * lap0))
+    yp1 = np.sqrt(1.0 / (1.0 / (T3 / np.sqrt(S1)) + gamma * lap1))
+    y0, y1 = np.sqrt(yobs[:, 0]), np.sqrt(yobs[:, 1])
+    diff = yp0 / y0 + y0 / yp0 + yp1 / y1 + y1 / yp1 - 4
+    return tau, dtau, ltau, diff
+
+
 def loss_n(diff, B_table, n_env, n_per_env):
     """loss_n (model_res_sigmoid_multi.py:947): sum(diff)/E/n + 0.01 ||B||^2 /E/n."""
     B = np.asarray(B_table, dtype=np.float64)

@@ -14,6 +14,9 @@ template <int DIM, int KIND>
 __global__ void field_kernel(FieldArgs a);
 template <int DIM>
 __global__ void plan_kernel(PlanArgs a);
+template <int DIM>
+__global__ void residual_kernel(ResidualArgs a);
+__global__ void sum_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ out);
 __global__ void pack_kernel(const float* __restrict__ src, int rows, int cols, int ld,
                             int trans, float* __restrict__ dst);
 __global__ void copy_kernel(const float* __restrict__ src, int n, float* __restrict__ dst);
@@ -237,6 +240,33 @@ int pntf_plan(const float* packed, int dim, const float* xp0, int64_t q, const f
   else
     hipLaunchKernelGGL((plan_kernel<6>), dim3((unsigned)grid), dim3(256), 0, stream, a);
   return check_launch("plan_kernel");
+}
+
+int pntf_eikonal_residual(const float* packed, int dim, const float* xp, const float* yobs,
+                          int64_t n, const float* Btab, const int32_t* env, int32_t n_env,
+                          float gamma, float* tau, float* dtau, float* ltau, float* diff,
+                          void* ws, size_t ws_bytes, hipStream_t stream) {
+  int st = check_common(packed, dim, xp, n, Btab, n_env);
+  if (st) return st;
+  if (n == 0) return PNTF_OK;
+  if (diff && !yobs) return fail(PNTF_ERR_ARG, "diff requested without yobs%s");
+  if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
+  int64_t grid;
+  st = grid_with_ws(n, ws_bytes, &grid);
+  if (st) return st;
+  ResidualArgs a{packed, xp, yobs, Btab, env, n, n_env, gamma, tau, dtau, ltau, diff,
+                 (float*)ws};
+  if (dim == 3)
+    hipLaunchKernelGGL((residual_kernel<3>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((residual_kernel<6>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+  return check_launch("residual_kernel");
+}
+
+int pntf_sum(const float* x, int64_t n, double* out, hipStream_t stream) {
+  if (!out || n < 0 || (n > 0 && !x)) return fail(PNTF_ERR_ARG, "bad pntf_sum arguments%s");
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, stream, x, n, out);
+  return check_launch("sum_kernel");
 }
 
 }  // extern "C"

@@ -99,4 +99,20 @@ struct PlanArgs {
   float* ws;
 };
 
+struct ResidualArgs {
+  const float* P;
+  const float* xp;       // (n, 2*DIM)
+  const float* yobs;     // (n, 2) observed speeds (may be null when diff is null)
+  const float* Btab;
+  const int32_t* env;
+  int64_t n;
+  int32_t n_env;
+  float gamma;           // viscosity weight of the Laplacian term (Model.Loss :937)
+  float* tau;            // (n)        optional
+  float* dtau;           // (n, 2*DIM) optional
+  float* ltau;           // (n, 2*DIM) optional: diagonal second derivatives
+  float* diff;           // (n)        optional: per-pair residual
+  float* ws;
+};
+
 }  // namespace pntf

@@ -166,8 +166,8 @@ constexpr int PF_STEPS = 3;
 // Generic layer: out tiles processed NO at a time (NO*NC >= 2 independent MFMA chains).
 //   init(ot, acc[o][c])  before the K loop of out-tile group starting at ot
 //   epi(ot, acc)         after it
-template <int OT, int KT, int NC, class InitF, class EpiF>
-__device__ __forceinline__ void layer(Rsrc W, int wbase, const f32x4 (&in)[16], int lane,
+template <int OT, int KT, int NC, int NIN, class InitF, class EpiF>
+__device__ __forceinline__ void layer(Rsrc W, int wbase, const f32x4 (&in)[NIN], int lane,
                                       InitF init, EpiF epi) {
   constexpr int NO = NC == 1 ? 2 : 1;
   constexpr int STEPS = (OT / NO) * KT;
@@ -749,6 +749,21 @@ __global__ void pack_kernel(const float* __restrict__ src, int rows, int cols, i
 __global__ void copy_kernel(const float* __restrict__ src, int n, float* __restrict__ dst) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] = src[i];
+}
+
+// Deterministic single-workgroup sum (fp64 accumulation) for loss_n.
+__global__ __launch_bounds__(1024) void sum_kernel(const float* __restrict__ x, int64_t n,
+                                                   double* __restrict__ out) {
+  __shared__ double part[1024];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) s += (double)x[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = part[0];
 }
 
 #endif  // PNTF_UTIL

@@ -1,13 +1,16 @@
 // One kernel per translation unit, selected at build time (pntf/build.py):
 //   -DPNTF_KIND=0..4 -DPNTF_DIM=3|6   field_kernel<DIM, KIND>
 //   -DPNTF_PLAN -DPNTF_DIM=3|6         plan_kernel<DIM>
-//   -DPNTF_UTIL                        pack_kernel, copy_kernel
-#include "pntf_field.h"
+//   -DPNTF_RESIDUAL -DPNTF_DIM=3|6     residual_kernel<DIM> (Taylor mode, pntf_taylor.h)
+//   -DPNTF_UTIL                        pack_kernel, copy_kernel, sum_kernel
+#include "pntf_taylor.h"
 
 namespace pntf {
 #if defined(PNTF_KIND)
 template __global__ void field_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
 #elif defined(PNTF_PLAN)
 template __global__ void plan_kernel<PNTF_DIM>(PlanArgs);
+#elif defined(PNTF_RESIDUAL)
+template __global__ void residual_kernel<PNTF_DIM>(ResidualArgs);
 #endif
 }  // namespace pntf

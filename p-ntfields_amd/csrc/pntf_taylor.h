@@ -1,0 +1,238 @@
+// Eikonal residual on MI355X: Taylor-mode (value, first and diagonal second derivative)
+// evaluation of the P-NTFields MLP and the per-pair residual of Model.Loss.
+//
+// Reference: NN.out_laplace (models/model_res_sigmoid_multi.py:710-848, helpers :649-708)
+// and Model.Loss (:897-951); restated in SURVEY.md Appendix A ("Taylor mode").
+//
+// Decomposition.  Per direction k (one coordinate of one endpoint) the Taylor rows
+// (J_k, L_k) obey, layer by layer,
+//     linear:  J' = A J,  L' = A L                        (+ residual J, L)
+//     act:     J = σ(y) J',  L = σ'(y) J'^2 + σ(y) L'    with σ' = 10 σ (1 - σ)
+// so directions never mix and need only σ(y) of the value pass.  The kernel therefore
+// runs the value pass once (field kernel forward, σ tiles saved to the wave's scratch
+// slot), then the 2·dim directions one after the other, each carrying (J_k, L_k) as two
+// MFMA column sets (NC = 2: one weight fragment feeds both) through encoder (the one
+// point the direction belongs to), merge, generator and head.  MACs per pair:
+// 40·128² (value) + 2·dim·2·(7 + 26)·128² = 436·128² for dim 3.
+#pragma once
+#include "pntf_field.h"
+
+namespace pntf {
+
+// (J, L) <- [act](A·(J, L) (+ residual)) with σ tiles sig0 + ot of the value pass.
+// in: J tiles in[0..KT), L tiles in[KT..2KT); out likewise with OT.
+template <int OT, int KT, bool RES, bool ACT, int NIN, int NOUT>
+__device__ __forceinline__ void taylor_layer(Rsrc W, int wbase, const f32x4 (&in)[NIN],
+                                             f32x4 (&out)[NOUT], Scratch sc, int sig0,
+                                             int lane) {
+  f32x4 g;
+  layer<OT, KT, 2>(
+      W, wbase, in, lane,
+      [&](int ot, f32x4 (&acc)[1][2]) {
+        if (ACT) g = load_tile(sc, sig0 + ot, lane);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[0][c] = RES ? out[c * OT + ot] : f32x4{0.f, 0.f, 0.f, 0.f};
+      },
+      [&](int ot, f32x4 (&acc)[1][2]) {
+        const f32x4 J = acc[0][0], L = acc[0][1];
+        if (ACT) {
+          const f32x4 gp = 10.f * g * (1.f - g);                     // DSigmoid (:89-96)
+          out[ot] = g * J;                                           // act_laplace :686
+          out[OT + ot] = gp * J * J + g * L;                         // :682-684
+        } else {
+          out[ot] = J;
+          out[OT + ot] = L;
+        }
+      });
+}
+
+// One direction k = p*DIM + d (p = 0 start, 1 goal point).  Returns (∂τ/∂x_k, ∂²τ/∂x_k²),
+// identical in all four lane groups.  TX/TY: 32-tile banks (J tiles 0..15, L tiles 16..31
+// in the generator; 0..7 / 8..15 in the encoder).
+template <int DIM>
+__device__ __forceinline__ void taylor_direction(Rsrc W, const PairIO& io, int p, int d,
+                                                 float tau, f32x4 (&TX)[32], f32x4 (&TY)[32],
+                                                 Scratch sc, int lane, float& Jt, float& Lt) {
+  const int g = lane >> 4;
+  constexpr int F = OFF_FWD * 4;
+  constexpr int BB = OFF_BIAS * 4;
+  float xp[DIM];
+#pragma unroll
+  for (int j = 0; j < DIM; ++j) xp[j] = p ? io.x[1][j] : io.x[0][j];
+
+  // ---- encoder[0] on the Fourier Jacobian / Hessian rows (input_mapping_laplace :199-213)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) TX[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    f32x4 js, jc, ls, lc;   // J/L rows of the sin part and the cos part of feature tile kt
+    pipelined<64, 2, PF_STEPS>(
+        W, lane * 16,
+        [&](int st, int l) { return frag<16>(F + OFF_E0 * 4, st % 8, st / 8 + 8 * l); },
+        [&](auto st, const f32x4 (&a)[2]) {
+          constexpr int kt = decltype(st)::value / 8, ot = decltype(st)::value % 8;
+          if constexpr (ot == 0) {
+            f32x4 q = f32x4{0.f, 0.f, 0.f, 0.f}, wd = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < DIM; ++j) {
+              f32x4 wj = TWO_PI * ld4(io.Bw + j * H + 16 * kt + 4 * g);
+              q += xp[j] * wj;
+              wd = (j == d) ? wj : wd;
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              float sn, cs;
+              sincos_fast(q[s], sn, cs);
+              js[s] = wd[s] * cs;
+              jc[s] = -wd[s] * sn;
+              ls[s] = -wd[s] * wd[s] * sn;
+              lc[s] = -wd[s] * wd[s] * cs;
+            }
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            TX[ot] = mfma(a[0][s], js[s], TX[ot]);
+            TX[8 + ot] = mfma(a[0][s], ls[s], TX[8 + ot]);
+            TX[ot] = mfma(a[1][s], jc[s], TX[ot]);
+            TX[8 + ot] = mfma(a[1][s], lc[s], TX[8 + ot]);
+          }
+        });
+  }
+#pragma unroll
+  for (int ot = 0; ot < 8; ++ot) {   // act_laplace of encoder[0] (:729)
+    const f32x4 gg = load_tile(sc, T_E0 + p * 8 + ot, lane);
+    const f32x4 gp = 10.f * gg * (1.f - gg);
+    const f32x4 J = TX[ot], L = TX[8 + ot];
+    TX[ot] = gg * J;
+    TX[8 + ot] = gp * J * J + gg * L;
+  }
+
+  // ---- encoder residual blocks (:731-746)
+#pragma unroll 1
+  for (int b = 0; b < 2; ++b) {
+    const int wa = opaque(F + (OFF_EBLK + (2 * b) * SZ_E) * 4);
+    const int wb = opaque(F + (OFF_EBLK + (2 * b + 1) * SZ_E) * 4);
+    taylor_layer<8, 8, false, true>(W, wa, TX, TY, sc, T_EBLK + 32 * b + p * 8, lane);
+    taylor_layer<8, 8, true, true>(W, wb, TY, TX, sc, T_EBLK + 32 * b + 16 + p * 8, lane);
+  }
+  // ---- encoder[-1], linear (:748-750) -> TY (J_z 0..7, L_z 8..15)
+  taylor_layer<8, 8, false, false>(W, F + OFF_E3 * 4, TX, TY, sc, 0, lane);
+
+  // ---- merge (:768-813): start directions take (s0, s1), goal directions (s1, s0)
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const f32x4 s0 = load_tile(sc, T_S0 + t, lane);
+    const f32x4 s1 = 1.f - s0;
+    const f32x4 c = 10.f * s0 * s1;                      // :790
+    const f32x4 a = p ? s1 : s0, bb = p ? s0 : s1;
+    const f32x4 J = TY[t], L = TY[8 + t];
+    const f32x4 cj = c * J * J;
+    TX[t] = a * J;               // J of the max half
+    TX[8 + t] = bb * J;          // J of the min half
+    TX[16 + t] = a * L + cj;     // L of the max half
+    TX[24 + t] = bb * L - cj;    // L of the min half
+  }
+
+  // ---- generator residual blocks (:816-829)
+#pragma unroll 1
+  for (int i = 0; i < 3; ++i) {
+    const int wa = opaque(F + (OFF_GBLK + (2 * i) * SZ_G) * 4);
+    const int wb = opaque(F + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4);
+    taylor_layer<16, 16, false, true>(W, wa, TX, TY, sc, T_GBLK + 32 * i, lane);
+    taylor_layer<16, 16, true, true>(W, wb, TY, TX, sc, T_GBLK + 32 * i + 16, lane);
+  }
+  // ---- generator[-2] + act (:832-835) -> TY (J_v 0..7, L_v 8..15)
+  taylor_layer<8, 16, false, true>(W, F + OFF_G3 * 4, TX, TY, sc, T_G3, lane);
+
+  // ---- head generator[-1] + actout_laplace (:837-840, :693-708)
+  float jy = 0.f, ly = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const f32x4 g4 = bload(W, g * 16, BB + (B_G4W + 16 * t) * 4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      jy = fmaf(g4[s], TY[t][s], jy);
+      ly = fmaf(g4[s], TY[8 + t][s], ly);
+    }
+  }
+  jy += __shfl_xor(jy, 16);
+  ly += __shfl_xor(ly, 16);
+  jy += __shfl_xor(jy, 32);
+  ly += __shfl_xor(ly, 32);
+  const float dt = 0.1f * tau * (1.f - tau);
+  const float ddt = 0.1f * dt * (1.f - 2.f * tau);
+  Jt = dt * jy;
+  Lt = ddt * jy * jy + dt * ly;
+}
+
+// Per-pair τ, ∇τ, Δ-rows and the Eikonal residual of Model.Loss (:914-946).
+template <int DIM>
+__device__ __forceinline__ void residual_body(const ResidualArgs& a, int slot, int nslots) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ntiles = (a.n + TILE - 1) / TILE;
+  const Scratch sc = make_scratch(a.ws + (int64_t)slot * SCRATCH_FLOATS_PER_WAVE);
+  const Rsrc W = make_rsrc(a.P, PACKED_FLOATS * 4);
+  const float nan = __builtin_nanf("");
+  for (int64_t tile = slot; tile < ntiles; tile += nslots) {
+    const int64_t pair = tile * TILE + (lane & 15);
+    PairIO io;
+    const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
+    const bool store = (lane < 16) && pair < a.n;
+    float tau;
+    {
+      f32x4 X[16], Y[16];
+      tau = forward_pass<DIM, true>(a.P, io, X, Y, sc, 0, lane);
+    }
+    drain_stores();
+    float D[DIM];
+    float T0 = 0.f;
+#pragma unroll
+    for (int j = 0; j < DIM; ++j) {
+      D[j] = io.x[1][j] - io.x[0][j];
+      T0 = fmaf(D[j], D[j], T0);
+    }
+    float d2[2] = {0.f, 0.f}, dD[2] = {0.f, 0.f}, lap[2] = {0.f, 0.f};
+#pragma unroll 1
+    for (int k = 0; k < 2 * DIM; ++k) {
+      const int p = k >= DIM ? 1 : 0;
+      const int d = k - p * DIM;
+      f32x4 TX[32], TY[32];
+      float Jt, Lt;
+      taylor_direction<DIM>(W, io, p, d, tau, TX, TY, sc, lane, Jt, Lt);
+      float Dd = 0.f;
+#pragma unroll
+      for (int j = 0; j < DIM; ++j) Dd = (j == d) ? D[j] : Dd;
+      // p is wave-uniform: select-accumulate keeps the arrays in registers
+      d2[0] += p ? 0.f : Jt * Jt;
+      d2[1] += p ? Jt * Jt : 0.f;
+      dD[0] += p ? 0.f : Jt * Dd;
+      dD[1] += p ? Jt * Dd : 0.f;
+      lap[0] += p ? 0.f : Lt;
+      lap[1] += p ? Lt : 0.f;
+      if (store) {
+        if (a.dtau) a.dtau[pair * 2 * DIM + k] = ok ? Jt : nan;
+        if (a.ltau) a.ltau[pair * 2 * DIM + k] = ok ? Lt : nan;
+      }
+    }
+    if (store) {
+      if (a.tau) a.tau[pair] = ok ? tau : nan;
+      if (a.diff) {
+        const float T3 = tau * tau;
+        const float S0 = T0 * d2[0] + 2.f * tau * dD[0] + T3;   // T01 - T02 + T3 (:925-933)
+        const float S1 = T0 * d2[1] - 2.f * tau * dD[1] + T3;   // T11 - T12 + T3
+        const float yp0 = 1.f / (sqrtf(S0) / T3 + a.gamma * lap[0]);   // :937-938
+        const float yp1 = 1.f / (sqrtf(S1) / T3 + a.gamma * lap[1]);
+        const float y0 = a.yobs[pair * 2], y1 = a.yobs[pair * 2 + 1];
+        const float df = yp0 / y0 + y0 / yp0 + yp1 / y1 + y1 / yp1 - 4.f;   // :943-946
+        a.diff[pair] = ok ? df : nan;
+      }
+    }
+  }
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256, WAVES_PER_SIMD) void residual_kernel(ResidualArgs a) {
+  residual_body<DIM>(a, blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                     gridDim.x * WAVES);
+}
+
+}  // namespace pntf

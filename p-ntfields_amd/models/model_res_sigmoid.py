@@ -62,7 +62,11 @@ class NN(torch.nn.Module):
         return t.unsqueeze(1), d, coords
 
     def out_laplace(self, coords):
-        raise NotImplementedError("NN.out_laplace is not on this round's HIP path yet")
+        """Taylor mode (models/model_res_sigmoid.py:676-826): coords (N, 2dim) ->
+        (τ (N,1), ∇τ (N,2dim), diagonal ∇²τ (N,2dim), coords)."""
+        out = ops.eikonal_residual(self.packed(), coords, self._B(coords.device), None,
+                                   self.dim, want=("tau", "dtau", "ltau"))
+        return out["tau"].unsqueeze(1), out["dtau"], out["ltau"], coords
 
     def forward(self, coords):
         coords = coords.clone().detach().requires_grad_(True)
@@ -84,6 +88,27 @@ class Model:
         grad_y = torch.ones_like(y)
         return torch.autograd.grad(y, x, grad_y, only_inputs=True, retain_graph=True,
                                    create_graph=create_graph)[0]
+
+    def Loss(self, points, Yobs, beta, gamma):
+        """The arm variant of the residual (models/model_res_sigmoid.py:869-935: square-root
+        speeds, viscosity on 1/Ypred).  τ, ∇τ and ∇²τ come from the HIP Taylor kernel; the
+        few elementwise epilogue ops run as device tensor ops.  Values only."""
+        tau, dtau, ltau, Xp = self.network.out_laplace(points)
+        d = self.dim
+        D = Xp[:, d:] - Xp[:, :d]
+        T0 = (D * D).sum(1)
+        lap0, lap1 = ltau[:, :d].sum(-1), ltau[:, d:].sum(-1)
+        DT0, DT1 = dtau[:, :d], dtau[:, d:]
+        t = tau[:, 0]
+        T3 = t * t
+        S0 = T0 * (DT0 * DT0).sum(1) + 2 * t * (DT0 * D).sum(1) + T3
+        S1 = T0 * (DT1 * DT1).sum(1) - 2 * t * (DT1 * D).sum(1) + T3
+        yp0 = torch.sqrt(1 / (torch.sqrt(S0) / T3 + gamma * lap0))
+        yp1 = torch.sqrt(1 / (torch.sqrt(S1) / T3 + gamma * lap1))
+        y0, y1 = torch.sqrt(Yobs[:, 0]), torch.sqrt(Yobs[:, 1])
+        diff = yp0 / y0 + y0 / yp0 + yp1 / y1 + y1 / yp1 - 4
+        loss_n = ops.device_sum(diff).float() / Yobs.shape[0]
+        return beta * loss_n, loss_n, diff
 
     def train(self):
         raise NotImplementedError("training is outside the HIP hot path of this round")

@@ -14,6 +14,9 @@ return shapes and state-dict keys are the reference's:
     Model(ModelPath, DataPath, dim, length, device)          :857-888
       .gradient(y, x)  .Gradient(Xp, B)  .Speed/.Tau/.TravelTimes(Xp)  .load  .save
 
+      .out_laplace(coords, B) -> (tau, dtau, ltau, coords)  :710-848 Taylor mode (HIP)
+    Model.Loss(points, Yobs, B, beta, gamma)  :897-951 Eikonal residual (HIP), values only
+
 Compute needs HIP device tensors; there is no CPU path (PntfError otherwise).  Training
 (`train`, `Loss`'s weight backward) and `plot` are outside this round's hot path and raise.
 """
@@ -65,6 +68,11 @@ def _as_table(B, device):
     if not isinstance(B, torch.Tensor):
         B = torch.as_tensor(np.asarray(B), dtype=torch.float32)
     return B.to(device=device, dtype=torch.float32)
+
+
+def _env_ids(E, n, device):
+    """env id of every flattened (E, n) pair."""
+    return torch.arange(E, device=device, dtype=torch.int32).repeat_interleave(n)
 
 
 class NN(torch.nn.Module):
@@ -119,9 +127,14 @@ class NN(torch.nn.Module):
         return t.unsqueeze(1), d, coords
 
     def out_laplace(self, coords, B):
-        raise NotImplementedError(
-            "NN.out_laplace (Taylor-mode Eikonal residual, :710-848) is not on this round's "
-            "HIP path yet")
+        """Taylor mode (:710-848): coords (E, n, 2dim), B (E, dim, 128) per env ->
+        (τ (E,n,1), ∇τ (E,n,2dim), diagonal ∇²τ (E,n,2dim), coords)."""
+        E, n, _ = coords.shape
+        out = ops.eikonal_residual(self.packed(), coords.reshape(E * n, -1),
+                                   _as_table(B, coords.device), _env_ids(E, n, coords.device),
+                                   self.dim, want=("tau", "dtau", "ltau"))
+        return (out["tau"].view(E, n, 1), out["dtau"].view(E, n, -1),
+                out["ltau"].view(E, n, -1), coords)
 
     def forward(self, coords, B, env=None):
         coords = coords.clone().detach().requires_grad_(True)
@@ -155,7 +168,18 @@ class Model:
                                    create_graph=create_graph)[0]
 
     def Loss(self, points, Yobs, B, beta, gamma):
-        raise NotImplementedError("Model.Loss needs NN.out_laplace (Eikonal residual)")
+        """Eikonal residual loss (:897-951): points (E,n,2dim), Yobs (E,n,2), B (E,dim,128).
+        Returns (loss, loss_n, diff (E,n)); the per-pair residual and its sum run on the
+        HIP kernels.  Values only: the weight gradient (training) is not on this path."""
+        E, n, _ = points.shape
+        dev = points.device
+        Bt = _as_table(B, dev)
+        out = ops.eikonal_residual(self.network.packed(), points.reshape(E * n, -1), Bt,
+                                   _env_ids(E, n, dev), self.dim,
+                                   yobs=Yobs.reshape(E * n, 2), gamma=gamma, want=("diff",))
+        diff = out["diff"].view(E, n)
+        loss_n = (ops.device_sum(diff) / E / n + 0.01 * ops.device_sum(Bt * Bt) / E / n).float()
+        return beta * loss_n, loss_n, diff
 
     def train(self):
         raise NotImplementedError("training (Model.train, :953-1141) is outside the HIP hot "

@@ -43,6 +43,11 @@ SIGNATURES = {
     "pntf_plan": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
                                  _c_void_p, _i32, ctypes.c_int, _f32, _f32, _i32, _c_void_p,
                                  _c_void_p, _c_void_p, _size, _c_void_p]),
+    "pntf_eikonal_residual": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _c_void_p,
+                                             _i64, _c_void_p, _c_void_p, _i32, _f32,
+                                             _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                             _c_void_p, _size, _c_void_p]),
+    "pntf_sum": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
 }
 
 _lib = None

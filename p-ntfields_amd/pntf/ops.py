@@ -12,8 +12,8 @@ from . import _lib
 from ._lib import GRAD_BACKGRAD_COMPAT, GRAD_EXACT, PntfError, check
 
 __all__ = ["GRAD_EXACT", "GRAD_BACKGRAD_COMPAT", "PntfError", "pack_weights", "tau",
-           "tau_grad", "path_velocity", "speed", "travel_time", "plan", "packed_floats",
-           "workspace_bytes"]
+           "tau_grad", "path_velocity", "speed", "travel_time", "plan", "eikonal_residual",
+           "device_sum", "packed_floats", "workspace_bytes"]
 
 _ws_cache = {}
 
@@ -170,3 +170,45 @@ def plan(packed, xp0, Btab, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
                         float(step), float(tol), int(max_iter), _vp(path), _vp(steps), _vp(ws),
                         ws.numel(), _stream(xp0.device)), "pntf_plan")
     return path, steps
+
+
+def eikonal_residual(packed, xp, Btab, env=None, dim=3, yobs=None, gamma=1e-3, want=("tau",
+                     "dtau", "ltau", "diff")):
+    """Taylor-mode τ, ∇τ, diagonal ∇²τ and the per-pair Eikonal residual of Model.Loss
+    (NN.out_laplace :710-848, Loss :914-946).  Returns a dict of the requested outputs."""
+    lib = _lib.load()
+    xp, Bt, env = _prep(xp, Btab, env, dim)
+    n = xp.shape[0]
+    dv = xp.device
+    out = {}
+    if "tau" in want:
+        out["tau"] = torch.empty(n, dtype=torch.float32, device=dv)
+    if "dtau" in want:
+        out["dtau"] = torch.empty((n, 2 * dim), dtype=torch.float32, device=dv)
+    if "ltau" in want:
+        out["ltau"] = torch.empty((n, 2 * dim), dtype=torch.float32, device=dv)
+    yo = None
+    if "diff" in want:
+        if yobs is None:
+            raise PntfError("the residual needs yobs (n, 2)")
+        _require_device(yobs, "yobs")
+        yo = yobs.detach().to(torch.float32).reshape(n, 2).contiguous()
+        out["diff"] = torch.empty(n, dtype=torch.float32, device=dv)
+    ws = _workspace(dv, n)
+    check(lib.pntf_eikonal_residual(_vp(packed), dim, _vp(xp), _vp(yo), n, _vp(Bt), _vp(env),
+                                    Bt.shape[0], float(gamma), _vp(out.get("tau")),
+                                    _vp(out.get("dtau")), _vp(out.get("ltau")),
+                                    _vp(out.get("diff")), _vp(ws), ws.numel(), _stream(dv)),
+          "pntf_eikonal_residual")
+    return out
+
+
+def device_sum(x):
+    """Deterministic fp64 sum of a float32 device tensor (pntf_sum); returns a 0-d float64
+    device tensor."""
+    lib = _lib.load()
+    _require_device(x, "x")
+    x = x.detach().to(torch.float32).contiguous().reshape(-1)
+    out = torch.empty((), dtype=torch.float64, device=x.device)
+    check(lib.pntf_sum(_vp(x), x.numel(), _vp(out), _stream(x.device)), "pntf_sum")
+    return out

@@ -168,6 +168,18 @@ def main():
                         tau=tau_a.detach().numpy(), dtau=dtau_a.detach().numpy(),
                         gradient16=grad_a, weight_checksum=csum, versions=versions)
 
+    # F5: arm Taylor mode + the arm loss variant (models/model_res_sigmoid.py:676-935)
+    nl = 64
+    pts_a = synth.make_box_pairs(nl, 6, seed=15)
+    yobs_a = synth.make_speeds(nl, seed=16)
+    tl, dl, ll, _ = anet.out_laplace(to_t(pts_a))
+    la, lna, dfa = amodel.Loss(to_t(pts_a), to_t(yobs_a), 1.0, 1e-3)
+    np.savez_compressed(os.path.join(args.out, "loss_d6.npz"), pts=pts_a, yobs=yobs_a, B=Ba,
+                        gamma=np.float64(1e-3), tau=tl.detach().numpy(),
+                        dtau=dl.detach().numpy(), ltau=ll.detach().numpy(),
+                        diff=dfa.detach().numpy(), loss_n=np.float64(lna.item()),
+                        weight_checksum=csum, versions=versions)
+
     base = np.array([[0, -0.5 * np.pi, 0.0, -0.5 * np.pi, 0.0, 0.0] * 2], np.float32)
     demo_a = np.array([[-2.2, 0.4, 1.1, 0.5, -0.5, 0.9, -1.3, 0.4, 1.1, 0.5, -0.5, 0.0]],
                       np.float32)                            # test/arm_plan.py:115-128

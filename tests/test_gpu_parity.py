@@ -232,3 +232,76 @@ def test_large_batch_properties(packed, dev):
     to, do = O.tau_grad(weights(), xp[idx], B)
     close(t[idx], to[:, 0])
     close(d[idx], do)
+
+
+# ---------------------------------------------------------------- Eikonal residual (A11)
+def test_out_laplace_and_loss_vs_reference(W, dev):
+    """NN.out_laplace + Model.Loss on the HIP Taylor kernel vs the reference goldens
+    (10 envs x 64 pairs, per-env B)."""
+    from models import model_res_sigmoid_multi as md
+    f = load("loss_d3.npz")
+    m = md.Model(".", ".", 3, 10, device="cuda")
+    m.network = md.NN("cuda", 3)
+    m.network.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m.network.to(dev)
+    pts, yobs, Bt = T(f["pts"], dev), T(f["yobs"], dev), T(f["B_table"], dev)
+    tau, dtau, ltau, _ = m.network.out_laplace(pts, Bt)
+    close(tau.cpu().numpy(), f["tau"])
+    close(dtau.cpu().numpy(), f["dtau"])
+    close(ltau.cpu().numpy(), f["ltau"])
+    loss, loss_n, diff = m.Loss(pts, yobs, Bt, 1.0, float(f["gamma"]))
+    close(diff.cpu().numpy(), f["diff"])
+    assert abs(float(loss_n) - float(f["loss_n"])) < 1e-4 * abs(float(f["loss_n"]))
+
+
+def test_arm_out_laplace_and_loss_vs_reference(W, dev):
+    from models import model_res_sigmoid as ma
+    f = load("loss_d6.npz")
+    m = ma.Model(".", ".", 6, device="cuda")
+    m.B = torch.from_numpy(f["B"])
+    m.network = ma.NN("cuda", 6, m.B)
+    m.network.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m.network.to(dev)
+    pts = T(f["pts"], dev)
+    tau, dtau, ltau, _ = m.network.out_laplace(pts)
+    close(tau.cpu().numpy(), f["tau"])
+    close(dtau.cpu().numpy(), f["dtau"])
+    close(ltau.cpu().numpy(), f["ltau"])
+    _, loss_n, diff = m.Loss(pts, T(f["yobs"], dev), 1.0, float(f["gamma"]))
+    close(diff.cpu().numpy(), f["diff"])
+
+
+@pytest.mark.parametrize("n", [1, 17, 300])
+def test_residual_ragged_vs_oracle(packed, dev, W, n):
+    xp = synth.make_pairs(n, 3, seed=300 + n)
+    Bt = synth.make_B_table(4, 3, first_seed=30)
+    env = synth.make_env_ids(n, 4, contiguous=False, seed=n)
+    yobs = synth.make_speeds(n, seed=n)
+    out = ops.eikonal_residual(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), 3,
+                               yobs=T(yobs, dev), gamma=1e-3)
+    to, do, lo, dfo = O.eikonal_residual(W, xp, yobs, Bt, env, gamma=1e-3)
+    close(out["tau"].cpu().numpy(), to[:, 0])
+    close(out["dtau"].cpu().numpy(), do)
+    close(out["ltau"].cpu().numpy(), lo)
+    close(out["diff"].cpu().numpy(), dfo)
+
+
+def test_residual_grad_agrees_with_reverse_sweep(packed, dev):
+    """Size-independent property at C3 scale (1M pairs): the forward-mode ∇τ of the Taylor
+    kernel equals the reverse-sweep ∇τ of the τ+∇τ kernel; τ is bit-identical."""
+    n = 1 << 20
+    xp = T(synth.make_pairs(n, 3, seed=2), dev)
+    Bt = T(synth.make_B_table(10, 3), dev)
+    env = T(synth.make_env_ids(n, 10), dev, torch.int32)
+    out = ops.eikonal_residual(packed, xp, Bt, env, 3, want=("tau", "dtau", "ltau"))
+    t, d = ops.tau_grad(packed, xp, Bt, env, dim=3)
+    assert torch.equal(out["tau"], t)
+    assert torch.isfinite(out["ltau"]).all()
+    close(out["dtau"].cpu().numpy(), d.cpu().numpy(), tol=1e-5)
+
+
+def test_device_sum_deterministic(dev):
+    x = torch.from_numpy(np.random.default_rng(0).standard_normal(1000003).astype(np.float32)).to(dev)
+    a, b = ops.device_sum(x), ops.device_sum(x)
+    assert a.item() == b.item()
+    assert abs(a.item() - float(x.double().sum())) < 1e-6 * float(x.abs().sum())

@@ -109,3 +109,15 @@ def test_planner_cap_semantics(W):
     path, steps = O.plan(W, xp0, B, step=1e-4, tol=1e-9, max_iter=3, compat=True)
     assert path.shape == (4, 5, 6)
     np.testing.assert_array_equal(steps, [4, 4, 4, 4])
+
+
+def test_arm_laplace_and_loss_variant(W):
+    f = load("loss_d6.npz")
+    B = f["B"].T
+    tau, dtau, ltau, diff = O.eikonal_residual_arm(W, f["pts"], f["yobs"], B, dim=6,
+                                                   gamma=float(f["gamma"]))
+    assert rel_l2(tau, f["tau"]) < TOL
+    assert rel_l2(dtau, f["dtau"]) < TOL
+    assert rel_l2(ltau, f["ltau"]) < 1e-4
+    assert rel_l2(diff, f["diff"]) < 1e-4
+    assert abs(diff.sum() / len(diff) - float(f["loss_n"])) < 1e-5

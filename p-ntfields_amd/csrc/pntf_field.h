@@ -69,6 +69,18 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 }
 
 // ---------------------------------------------------------------- weight stream
+// Weight-stream prefetch depth (steps of the pipelined ring), step fences (bitmask of SITE_*
+// call sites) and out tiles per MFMA group for single-column layers; overridable for the
+// perf-variant diagnostics (tests/diag).
+#ifndef PNTF_PF_STEPS
+#define PNTF_PF_STEPS 3
+#endif
+#ifndef PNTF_STEP_FENCE
+#define PNTF_STEP_FENCE 127
+#endif
+#ifndef PNTF_NO1
+#define PNTF_NO1 4
+#endif
 // Packed weights are read through a buffer resource: per-lane voffset = lane*16 and a
 // scalar byte offset per fragment, so address math stays on the SALU.
 typedef __amdgpu_buffer_rsrc_t Rsrc;
@@ -93,7 +105,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 // Software-pipelined step sequence: step st consumes NL weight fragments whose byte offsets
 // are addr(st, l); fragments are prefetched PF steps ahead into a register ring so the
 // L2/MALL latency of the stream hides behind the MFMAs of the previous PF steps.
-template <int STEPS, int NL, int PF, class AddrF, class BodyF>
+template <int STEPS, int NL, int PF, int SITE, class AddrF, class BodyF>
 __device__ __forceinline__ void pipelined(Rsrc r, int voff, AddrF addr, BodyF body) {
   f32x4 ring[PF][NL];
   static_for<0, (PF < STEPS ? PF : STEPS)>([&](auto p) {
@@ -110,6 +122,9 @@ __device__ __forceinline__ void pipelined(Rsrc r, int voff, AddrF addr, BodyF bo
       for (int l = 0; l < NL; ++l) ring[S % PF][l] = bload(r, voff, addr(S + PF, l));
     }
     body(st, a);
+    // Keep every load in the step that issues it: without the fence the scheduler sinks
+    // prefetches next to their MFMA under register pressure, collapsing the ring.
+    if constexpr ((PNTF_STEP_FENCE & SITE) != 0) __builtin_amdgcn_sched_barrier(0);
   });
 }
 
@@ -161,18 +176,36 @@ __device__ __forceinline__ f32x4 load_tile(Scratch sc, int tile, int lane) {
 // under full-chip load (measured: garbage ∇τ rows at 262k pairs, 2 workgroups per CU).
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-constexpr int PF_STEPS = 3;
+// Diagnostics only (tests/diag): -DPNTF_DEBUG_DUMP writes intermediate tiles of each wave's
+// last pair tile to pntf_dbg[(wave*64 + idx)*256 + lane*4 ..].  Never in the shipped library.
+#ifdef PNTF_DEBUG_DUMP
+__device__ float* pntf_dbg;
+__device__ __forceinline__ void dbg_tile(int idx, int lane, f32x4 v) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  *reinterpret_cast<f32x4*>(pntf_dbg + ((size_t)w * 64 + idx) * 256 + lane * 4) = v;
+}
+#define PNTF_DBG(idx, v) dbg_tile(idx, lane, v)
+#else
+#define PNTF_DBG(idx, v)
+#endif
+
+constexpr int PF_STEPS = PNTF_PF_STEPS;
+// Pipelined call sites (bits of PNTF_STEP_FENCE).
+constexpr int SITE_FWD_E0 = 1, SITE_FWD_ENC = 2, SITE_FWD_GEN = 4, SITE_BWD_GEN = 8,
+              SITE_BWD_ENC = 16, SITE_FOLD = 32, SITE_TAYLOR = 64;
+template <int NC>
+constexpr int out_group() { return NC == 1 ? PNTF_NO1 : 1; }
 
 // Generic layer: out tiles processed NO at a time (NO*NC >= 2 independent MFMA chains).
 //   init(ot, acc[o][c])  before the K loop of out-tile group starting at ot
 //   epi(ot, acc)         after it
-template <int OT, int KT, int NC, int NIN, class InitF, class EpiF>
+template <int OT, int KT, int NC, int SITE, int NIN, class InitF, class EpiF>
 __device__ __forceinline__ void layer(Rsrc W, int wbase, const f32x4 (&in)[NIN], int lane,
                                       InitF init, EpiF epi) {
-  constexpr int NO = NC == 1 ? 2 : 1;
+  constexpr int NO = out_group<NC>();
   constexpr int STEPS = (OT / NO) * KT;
   f32x4 acc[NO][NC];
-  pipelined<STEPS, NO, PF_STEPS>(
+  pipelined<STEPS, NO, PF_STEPS, SITE>(
       W, lane * 16,
       [&](int st, int l) { return frag<KT>(wbase, (st / KT) * NO + l, st % KT); },
       [&](auto st, const f32x4 (&a)[NO]) {
@@ -195,9 +228,9 @@ template <int OT, int KT, int NC, bool RES, bool SAVE>
 __device__ __forceinline__ void fwd_act_layer(Rsrc W, int wbase, int bias,
                                               const f32x4 (&in)[16], f32x4 (&out)[16],
                                               Scratch sc, int sc0, int lane) {
-  constexpr int NO = NC == 1 ? 2 : 1;
+  constexpr int NO = out_group<NC>();
   const int g = lane >> 4;
-  layer<OT, KT, NC>(
+  layer<OT, KT, NC, NC == 2 ? SITE_FWD_ENC : SITE_FWD_GEN>(
       W, wbase, in, lane,
       [&](int ot, f32x4 (&acc)[NO][NC]) {
 #pragma unroll
@@ -230,9 +263,9 @@ template <int OT, int KT, int NC>
 __device__ __forceinline__ void fwd_lin_layer(Rsrc W, int wbase, int bias,
                                               const f32x4 (&in)[16], f32x4 (&out)[16],
                                               int lane) {
-  constexpr int NO = NC == 1 ? 2 : 1;
+  constexpr int NO = out_group<NC>();
   const int g = lane >> 4;
-  layer<OT, KT, NC>(
+  layer<OT, KT, NC, NC == 2 ? SITE_FWD_ENC : SITE_FWD_GEN>(
       W, wbase, in, lane,
       [&](int ot, f32x4 (&acc)[NO][NC]) {
 #pragma unroll
@@ -256,9 +289,9 @@ template <int OT, int KT, int NC, bool RES, bool MUL>
 __device__ __forceinline__ void bwd_layer(Rsrc W, int wbase, const f32x4 (&in)[16],
                                           f32x4 (&out)[16], Scratch sc,
                                           int mul0, int lane) {
-  constexpr int NO = NC == 1 ? 2 : 1;
+  constexpr int NO = out_group<NC>();
   f32x4 m[NO][NC];
-  layer<OT, KT, NC>(
+  layer<OT, KT, NC, NC == 2 ? SITE_BWD_ENC : SITE_BWD_GEN>(
       W, wbase, in, lane,
       [&](int ot, f32x4 (&acc)[NO][NC]) {
 #pragma unroll
@@ -325,7 +358,7 @@ __device__ __forceinline__ float forward_pass(const float* __restrict__ P, const
   }
   {
     f32x4 sn[2], cs[2];
-    pipelined<64, 2, PF_STEPS>(
+    pipelined<64, 2, PF_STEPS, SITE_FWD_E0>(
         W, lane * 16,
         [&](int st, int l) { return frag<16>(F + OFF_E0 * 4, st % 8, st / 8 + 8 * l); },
         [&](auto st, const f32x4 (&a)[2]) {
@@ -363,6 +396,8 @@ __device__ __forceinline__ float forward_pass(const float* __restrict__ P, const
     }
     X[i] = s;
     if (GRAD) store_tile(sc, T_E0 + i, lane, sg);
+    PNTF_DBG(i, sg);
+    PNTF_DBG(16 + i, s);
   }
 
   // ---- encoder residual blocks (:228-232); X = h (2 cols x 8 tiles)
@@ -482,9 +517,11 @@ __device__ __forceinline__ void backward_pass(const float* __restrict__ P, const
   // Step (kf, kt) loads fragments (kf, kt) [dφ_sin rows] and (kf + 8, kt) [dφ_cos rows].
   float acc[2][DIM];
 #pragma unroll
+  for (int i = 0; i < 16; ++i) PNTF_DBG(32 + i, Y[i]);
+#pragma unroll
   for (int d = 0; d < DIM; ++d) acc[0][d] = acc[1][d] = 0.f;
   f32x4 ph[2][2];
-  pipelined<64, 2, PF_STEPS>(
+  pipelined<64, 2, PF_STEPS, SITE_FOLD>(
       W, lane * 16,
       [&](int st, int l) { return frag<8>(Bk + OFF_E0 * 4, st / 8 + 8 * l, st % 8); },
       [&](auto st, const f32x4 (&a)[2]) {
@@ -520,10 +557,12 @@ __device__ __forceinline__ void backward_pass(const float* __restrict__ P, const
 #pragma unroll
   for (int d = 0; d < DIM; ++d) {
     float a0 = acc[0][d], a1 = acc[1][d];
+    PNTF_DBG(48 + d, (f32x4{a0, a1, 0.f, 0.f}));
     a0 += __shfl_xor(a0, 16);
     a1 += __shfl_xor(a1, 16);
     a0 += __shfl_xor(a0, 32);
     a1 += __shfl_xor(a1, 32);
+    PNTF_DBG(56 + d, (f32x4{a0, a1, 0.f, 0.f}));
     ds[d] = a0;
     dg[d] = a1;
   }

@@ -26,7 +26,7 @@ __device__ __forceinline__ void taylor_layer(Rsrc W, int wbase, const f32x4 (&in
                                              f32x4 (&out)[NOUT], Scratch sc, int sig0,
                                              int lane) {
   f32x4 g;
-  layer<OT, KT, 2>(
+  layer<OT, KT, 2, SITE_TAYLOR>(
       W, wbase, in, lane,
       [&](int ot, f32x4 (&acc)[1][2]) {
         if (ACT) g = load_tile(sc, sig0 + ot, lane);
@@ -65,7 +65,7 @@ __device__ __forceinline__ void taylor_direction(Rsrc W, const PairIO& io, int p
   for (int i = 0; i < 16; ++i) TX[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     f32x4 js, jc, ls, lc;   // J/L rows of the sin part and the cos part of feature tile kt
-    pipelined<64, 2, PF_STEPS>(
+    pipelined<64, 2, PF_STEPS, SITE_TAYLOR>(
         W, lane * 16,
         [&](int st, int l) { return frag<16>(F + OFF_E0 * 4, st % 8, st / 8 + 8 * l); },
         [&](auto st, const f32x4 (&a)[2]) {

@@ -2,14 +2,27 @@
 
     python -m pntf.build [--jobs N] [--force]
 
-Objects go to p-ntfields_amd/build/ (git-ignored); the shared library lands next to this
-file (p-ntfields_amd/pntf/libpntf.so) so it travels with the repo snapshot to the GPU box.
-A stamp of the sources and flags skips the rebuild when nothing changed.
+Objects go to p-ntfields_amd/build/<unit>/ (git-ignored) with the device assembly kept
+beside them; the shared library lands next to this file (p-ntfields_amd/pntf/libpntf.so) so
+it travels with the repo snapshot to the GPU box.  A stamp of the sources and flags skips the
+rebuild when nothing changed.
+
+Two codegen guards fail the build instead of shipping a wrong kernel:
+  * no VGPR spills (a spilling build of the field kernel corrupted results, DESIGN.md §7);
+  * no packed-fp32 VALU ops (v_pk_{mul,add,fma}_f32) in device code.  On gfx950 a packed op
+    that reads the result of a transcendental (v_exp/v_log/v_rcp/v_sin/v_cos) issued a few
+    instructions earlier sees stale values in lanes 12-15 of every 16-lane row; ROCm 7.2's
+    hazard recognizer under-pads that pair (measured: tests/diag).  Packed-fp32
+    codegen is therefore disabled for the device (-packed-fp32-ops), which costs nothing here.
+A summary of every kernel's registers and spills is written to build/report.json.
 """
 import argparse
 import concurrent.futures as cf
+import glob
 import hashlib
+import json
 import os
+import re
 import subprocess
 import sys
 
@@ -23,7 +36,10 @@ LIB = os.path.join(PKG, "libpntf.so")
 
 ARCH = "gfx950"
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + INCLUDE,
-            "-I" + CSRC, "-Wno-unused-result"]
+            "-I" + CSRC, "-Wno-unused-result",
+            "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
+            "-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"]
+PACKED_FP32 = re.compile(r"\bv_pk_(mul|add|fma)_f32\b")
 
 UNITS = (
     [("field_d%d_k%d" % (d, k), "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k])
@@ -52,14 +68,44 @@ def _stamp():
     return h.hexdigest()
 
 
+def _resources(stderr):
+    """Per-kernel register / spill figures from -Rpass-analysis=kernel-resource-usage."""
+    out, cur = {}, None
+    for line in stderr.splitlines():
+        m = re.search(r"remark:.*Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:.*?\s(VGPRs|AGPRs|TotalSGPRs|VGPRs Spill|SGPRs Spill|"
+                      r"ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\d+) ", line)
+        if m and cur is not None:
+            cur[m.group(1)] = int(m.group(2))
+    return out
+
+
 def _compile(unit):
     name, src, defs = unit
-    obj = os.path.join(BUILD, name + ".o")
+    d = os.path.join(BUILD, name)
+    os.makedirs(d, exist_ok=True)
+    obj = os.path.join(d, name + ".o")
     cmd = [hipcc()] + CXXFLAGS + defs + ["-c", os.path.join(CSRC, src), "-o", obj]
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd=d)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (name, " ".join(cmd), r.stderr))
-    return obj
+    res = _resources(r.stderr)
+    bad = {k: v for k, v in res.items() if v.get("VGPRs Spill", 0) or v.get(
+        "ScratchSize [bytes/lane]", 0)}
+    if bad:
+        raise RuntimeError("VGPR spills / scratch in %s: %s" % (name, bad))
+    for asm in glob.glob(os.path.join(d, "*amdgcn*gfx950*.s")):
+        with open(asm) as fh:
+            m = PACKED_FP32.search(fh.read())
+        if m:
+            raise RuntimeError("packed-fp32 op %s in %s (hazard guard)" % (m.group(0), asm))
+    for f in glob.glob(os.path.join(d, "*")):
+        if not f.endswith((".o", ".s")):
+            os.remove(f)
+    return obj, {name + ":" + k: v for k, v in res.items()}
 
 
 def build(jobs=None, force=False, verbose=True):
@@ -76,7 +122,13 @@ def build(jobs=None, force=False, verbose=True):
     if verbose:
         print("building libpntf.so (%d units, %d jobs, %s)" % (len(UNITS), jobs, ARCH))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(_compile, UNITS))
+        results = list(ex.map(_compile, UNITS))
+    objs = [o for o, _ in results]
+    report = {}
+    for _, res in results:
+        report.update(res)
+    with open(os.path.join(BUILD, "report.json"), "w") as fh:
+        json.dump(report, fh, indent=1, sort_keys=True)
     tmp = LIB + ".tmp"
     cmd = [hipcc(), "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)

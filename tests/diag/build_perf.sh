@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build perf variants of the τ+∇τ kernel: name=flags pairs; prints each one's resource usage.
+set -e
+cd "$(dirname "$0")/../.."
+build() {
+  local name=$1; shift
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -Iinclude \
+    -Ip-ntfields_amd/csrc "$@" tests/diag/perf_variant.hip -o tests/diag/libperf_$name.so \
+    -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "VGPRs:|AGPRs|Spill" | tr '\n' ' ' \
+    | sed "s/^/$name: /"; echo
+}
+for v in "$@"; do
+  name=${v%%=*}; flags=${v#*=}
+  build $name $flags &
+done
+wait

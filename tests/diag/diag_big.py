@@ -1,6 +1,6 @@
 """Diagnostic: full-chip ∇τ repeatability and oracle agreement at 262k pairs."""
 import sys, os
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "p-ntfields_amd")]
 import numpy as np, torch
 from pntf import ops, synth

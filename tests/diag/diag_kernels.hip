@@ -1,5 +1,5 @@
 // Diagnostic builds of the τ+∇τ kernel body under other launch bounds / workgroup shapes.
-// Not part of libpntf.so; built by tools/diag_build.sh into tools/libdiag.so.
+// Not part of libpntf.so; built by hand with hipcc -shared into tests/diag/libdiag.so.
 #include "pntf_field.h"
 
 namespace pntf {

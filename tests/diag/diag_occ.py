@@ -1,6 +1,6 @@
 """Diagnostic: ∇τ errors vs grid size at 262k pairs (1 vs 2 workgroups per CU)."""
 import ctypes, sys, os
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "p-ntfields_amd")]
 import numpy as np, torch
 from pntf import ops, synth, _lib

@@ -1,6 +1,6 @@
 """Diagnostic: ∇τ correctness vs tiles-per-wave (workspace-limited grid)."""
 import ctypes, sys, os
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "p-ntfields_amd")]
 import numpy as np, torch
 from pntf import ops, synth, _lib

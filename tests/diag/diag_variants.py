@@ -1,6 +1,6 @@
-"""Diagnostic: ∇τ errors at 262k pairs for launch-bound / occupancy variants (tools/libdiag.so)."""
+"""Diagnostic: ∇τ errors at 262k pairs for launch-bound / occupancy variants (tests/diag/libdiag.so)."""
 import ctypes, sys, os
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "p-ntfields_amd")]
 import numpy as np, torch
 from pntf import ops, synth
@@ -8,7 +8,7 @@ from oracle import pntf_oracle as O
 dev = torch.device("cuda:0")
 W = synth.make_weights(0)
 packed = ops.pack_weights([torch.from_numpy(v).to(dev) for v in W.values()])
-lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libdiag.so"))
+lib = ctypes.CDLL(os.path.join(ROOT, "tests", "diag", "libdiag.so"))
 n = 262144
 xp = synth.make_pairs(n, 3, seed=2); B = synth.make_B(3, seed=1)
 idx = np.arange(0, n, 97)

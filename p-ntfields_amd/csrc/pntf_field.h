@@ -11,8 +11,19 @@
 // the A operand and the previous layer's output tiles as the B operand.  The forward
 // pass stores σ10(pre-activation) tiles to a per-wave scratch slot that the analytic
 // reverse sweep reads back; nothing crosses waves, so there is no LDS and no barrier.
-// Workgroups (4 waves) are persistent, two per CU (two waves per SIMD), and loop over
-// pair tiles.
+// Workgroups (4 waves, one per SIMD) are persistent and loop over pair tiles.
+//
+// Pipeline structure:
+//   * one weight-fragment prefetch ring (Ring) flows through the whole pair tile: the last
+//     PF steps of every layer prefetch the first PF steps of the layer after it, and the
+//     last layer of a tile prefetches the first layer of the next tile;
+//   * every layer's epilogue (bias, softplus, σ store / σ multiply) is deferred: the
+//     epilogue of out-tile group g runs inside the first steps of group g+1, and the last
+//     group's epilogue inside the first steps of the next layer where that layer does not
+//     need it yet, so the VALU work issues in the shadow of MFMAs;
+//   * a group's bias / saved-σ tiles are loaded when the group starts and consumed by its
+//     deferred epilogue a group later (double-buffered by group parity), so no load is
+//     consumed right after it issues.
 #include <type_traits>
 
 #include "pntf_common.h"
@@ -35,13 +46,19 @@ struct SpSig {
   float sp, sg;
 };
 __device__ __forceinline__ SpSig sp_sig(float y) {
+#ifdef PNTF_ABL_CHEAPACT   // diagnostics only (tests/diag ablations): no transcendentals
+  return SpSig{fmaxf(y, 0.f) * 0.5f + 0.01f, 0.5f};
+#endif
   float t = exp_neg10abs(y);
-  float r = __builtin_amdgcn_rcpf(1.f + t);
+  float u = 1.f + t;
+  float r = __builtin_amdgcn_rcpf(u);
+  bool pos = y >= 0.f;
   SpSig o;
-  // torch returns y itself above 10y > 20; there 0.1*log1p(t) < 2.1e-10 < ulp(y)/2, so the
-  // same expression rounds to exactly y without a select.
-  o.sp = fmaxf(y, 0.f) + 0.1f * log1p_small(t);
-  o.sg = (y >= 0.f) ? r : t * r;
+  // softplus_10(y) = max(y, 0) + log(1 + e^{-10|y|}) / 10, with log2 → ln and the 1/10
+  // folded into one constant.  torch returns y itself above 10y > 20; there the log term is
+  // < 2.1e-10 < ulp(y)/2, so the same expression rounds to exactly y without a select.
+  o.sp = fmaf(__builtin_amdgcn_logf(u), 0.0693147180559945309f, pos ? y : 0.f);
+  o.sg = pos ? r : t * r;
   return o;
 }
 
@@ -68,18 +85,23 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
 // ---------------------------------------------------------------- weight stream
-// Weight-stream prefetch depth (steps of the pipelined ring), step fences (bitmask of SITE_*
-// call sites) and out tiles per MFMA group for single-column layers; overridable for the
+// Weight-stream prefetch depth (steps of the ring), step fences (bitmask of SITE_* call
+// sites) and out tiles per MFMA group for single-column layers; overridable for the
 // perf-variant diagnostics (tests/diag).
 #ifndef PNTF_PF_STEPS
-#define PNTF_PF_STEPS 3
+#define PNTF_PF_STEPS 4
 #endif
 #ifndef PNTF_STEP_FENCE
 #define PNTF_STEP_FENCE 127
 #endif
 #ifndef PNTF_NO1
 #define PNTF_NO1 4
+#endif
+#ifndef PNTF_IGLP_V
+#define PNTF_IGLP_V 0
 #endif
 // Packed weights are read through a buffer resource: per-lane voffset = lane*16 and a
 // scalar byte offset per fragment, so address math stays on the SALU.
@@ -102,30 +124,90 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// Software-pipelined step sequence: step st consumes NL weight fragments whose byte offsets
-// are addr(st, l); fragments are prefetched PF steps ahead into a register ring so the
-// L2/MALL latency of the stream hides behind the MFMAs of the previous PF steps.
-template <int STEPS, int NL, int PF, int SITE, class AddrF, class BodyF>
-__device__ __forceinline__ void pipelined(Rsrc r, int voff, AddrF addr, BodyF body) {
-  f32x4 ring[PF][NL];
-  static_for<0, (PF < STEPS ? PF : STEPS)>([&](auto p) {
-#pragma unroll
-    for (int l = 0; l < NL; ++l) ring[p][l] = bload(r, voff, addr(p(), l));
-  });
+constexpr int PF_STEPS = PNTF_PF_STEPS;
+constexpr int RING_NL = 4;   // fragments per step, at most
+// Pipelined call sites (bits of PNTF_STEP_FENCE).
+constexpr int SITE_FWD_E0 = 1, SITE_FWD_ENC = 2, SITE_FWD_GEN = 4, SITE_BWD_GEN = 8,
+              SITE_BWD_ENC = 16, SITE_FOLD = 32, SITE_TAYLOR = 64;
+
+// The weight-fragment prefetch ring: slot j % PF holds the fragments of step j for the PF
+// steps ahead of the one being computed.
+struct Ring {
+  f32x4 r[PF_STEPS][RING_NL];
+};
+
+// "Nothing follows": the ring drains at the end of the step sequence.
+struct NoNext {
+  __device__ int operator()(int, int) const { return 0; }
+};
+// First steps of a standard layer with KT input tiles and KS k-tiles per step: step j < PF
+// reads fragment l = o*KS + ks = (out tile o, k tile j*KS + ks).
+template <int KT, int KS = 1>
+struct Head {
+  int base;
+  __device__ int operator()(int j, int l) const {
+    return base + (((l / KS) * KT + j * KS + l % KS) * 64) * 16;
+  }
+};
+
+// Byte offset of fragment (ot, kt) of a packed (OT x KT) layer.
+template <int KT>
+__device__ __forceinline__ int frag(int base, int ot, int kt) {
+  return base + ((ot * KT + kt) * 64) * 16;
+}
+
+// Software-pipelined step sequence.  Step st consumes NL weight fragments whose byte offsets
+// are addr(st, l).  On entry the ring holds steps 0..PF-1; the last PF steps refill it with
+// the first PF steps of whatever follows (naddr, NLN fragments per step), so the L2 latency
+// of the stream stays hidden across layer boundaries.
+template <int STEPS, int NL, int NLN, int SITE, class AddrF, class NextF, class BodyF>
+__device__ __forceinline__ void run_steps(Ring& ring, Rsrc r, int voff, AddrF addr,
+                                          NextF naddr, BodyF body) {
+  static_assert(STEPS % PF_STEPS == 0, "step count must be a multiple of the ring depth");
+  static_assert(NL <= RING_NL && NLN <= RING_NL, "ring width");
   static_for<0, STEPS>([&](auto st) {
     constexpr int S = decltype(st)::value;
+    constexpr int slot = S % PF_STEPS;
     f32x4 a[NL];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) a[l] = ring[S % PF][l];
-    if constexpr (S + PF < STEPS) {
+    for (int l = 0; l < NL; ++l) a[l] = ring.r[slot][l];
+    if constexpr (S + PF_STEPS < STEPS) {
 #pragma unroll
-      for (int l = 0; l < NL; ++l) ring[S % PF][l] = bload(r, voff, addr(S + PF, l));
+      for (int l = 0; l < NL; ++l) ring.r[slot][l] = bload(r, voff, addr(S + PF_STEPS, l));
+    } else {
+#pragma unroll
+      for (int l = 0; l < NLN; ++l)
+        ring.r[slot][l] = bload(r, voff, naddr(S + PF_STEPS - STEPS, l));
     }
     body(st, a);
+#if PNTF_IGLP_V > 0
+    // Interleave the step as (1 MFMA, PNTF_IGLP_V VALU) x 16 so dependent VALU chains of the
+    // deferred epilogues sit between MFMAs instead of stalling the wave's in-order issue.
+    static_for<0, 16>([&](auto) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, PNTF_IGLP_V, 0);
+    });
+#endif
     // Keep every load in the step that issues it: without the fence the scheduler sinks
     // prefetches next to their MFMA under register pressure, collapsing the ring.
     if constexpr ((PNTF_STEP_FENCE & SITE) != 0) __builtin_amdgcn_sched_barrier(0);
   });
+}
+
+template <int NL, class AddrF>
+__device__ __forceinline__ void ring_fill(Ring& ring, Rsrc r, int voff, AddrF addr) {
+#pragma unroll
+  for (int p = 0; p < PF_STEPS; ++p)
+#pragma unroll
+    for (int l = 0; l < NL; ++l) ring.r[p][l] = bload(r, voff, addr(p, l));
+}
+
+// Standalone step sequence with its own ring (filled on entry, drained at the end).
+template <int STEPS, int NL, int SITE, class AddrF, class BodyF>
+__device__ __forceinline__ void pipelined(Rsrc r, int voff, AddrF addr, BodyF body) {
+  Ring ring;
+  ring_fill<NL>(ring, r, voff, addr);
+  run_steps<STEPS, NL, 0, SITE>(ring, r, voff, addr, NoNext{}, body);
 }
 
 // Hide a wave-uniform integer from the optimizer: inside the runtime block loops this keeps
@@ -134,12 +216,6 @@ __device__ __forceinline__ void pipelined(Rsrc r, int voff, AddrF addr, BodyF bo
 __device__ __forceinline__ int opaque(int x) {
   asm volatile("" : "+s"(x));
   return x;
-}
-
-// Byte offset of fragment (ot, kt) of a packed (OT x KT) layer.
-template <int KT>
-__device__ __forceinline__ int frag(int base, int ot, int kt) {
-  return base + ((ot * KT + kt) * 64) * 16;
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) {
@@ -162,159 +238,235 @@ __device__ __forceinline__ Scratch make_scratch(float* sc) {
   return Scratch{make_rsrc(sc, sc ? SCRATCH_FLOATS_PER_WAVE * 4 : 0)};
 }
 __device__ __forceinline__ void store_tile(Scratch sc, int tile, int lane, f32x4 v) {
+#ifdef PNTF_ABL_NOSTORE   // diagnostics only (tests/diag ablations)
+  asm volatile("" ::"v"(v));
+  return;
+#endif
   __builtin_amdgcn_raw_buffer_store_b128(
       __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), sc.r, lane * 16,
       tile * 1024, AUX_NT);
 }
 __device__ __forceinline__ f32x4 load_tile(Scratch sc, int tile, int lane) {
+#ifdef PNTF_ABL_NOLOAD    // diagnostics only (tests/diag ablations)
+  return f32x4{0.5f, 0.5f, 0.5f, 0.5f};
+#endif
   return __builtin_bit_cast(
       f32x4, __builtin_amdgcn_raw_buffer_load_b128(sc.r, lane * 16, tile * 1024, AUX_NT));
 }
 // Between the forward sweep (stores) and the reverse sweep (loads of the same slot): wait
 // until every store of this wave has been performed.  Without it the first reverse-sweep
-// loads (the G3 σ tiles, stored a few hundred cycles earlier) can overtake their stores
-// under full-chip load (measured: garbage ∇τ rows at 262k pairs, 2 workgroups per CU).
+// loads (stored a few hundred cycles earlier) can overtake their stores under full-chip
+// load (measured: garbage ∇τ rows at 262k pairs, 2 workgroups per CU).
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Diagnostics only (tests/diag): -DPNTF_DEBUG_DUMP writes intermediate tiles of each wave's
-// last pair tile to pntf_dbg[(wave*64 + idx)*256 + lane*4 ..].  Never in the shipped library.
-#ifdef PNTF_DEBUG_DUMP
-__device__ float* pntf_dbg;
-__device__ __forceinline__ void dbg_tile(int idx, int lane, f32x4 v) {
-  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  *reinterpret_cast<f32x4*>(pntf_dbg + ((size_t)w * 64 + idx) * 256 + lane * 4) = v;
-}
-#define PNTF_DBG(idx, v) dbg_tile(idx, lane, v)
+// Diagnostics only (tests/diag/stamps.py): -DPNTF_DEBUG_STAMPS records s_memtime at phase
+// boundaries into pntf_stamps[wave*64 + idx] (each tile overwrites: the last tile remains).
+#ifdef PNTF_DEBUG_STAMPS
+__device__ unsigned long long* pntf_stamps;
+#define PNTF_STAMP(idx)                                                                  \
+  do {                                                                                   \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();                                \
+    if ((threadIdx.x & 63) == 0)                                                         \
+      pntf_stamps[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + (idx)] = _t;              \
+  } while (0)
 #else
-#define PNTF_DBG(idx, v)
+#define PNTF_STAMP(idx)
 #endif
 
-constexpr int PF_STEPS = PNTF_PF_STEPS;
-// Pipelined call sites (bits of PNTF_STEP_FENCE).
-constexpr int SITE_FWD_E0 = 1, SITE_FWD_ENC = 2, SITE_FWD_GEN = 4, SITE_BWD_GEN = 8,
-              SITE_BWD_ENC = 16, SITE_FOLD = 32, SITE_TAYLOR = 64;
 template <int NC>
 constexpr int out_group() { return NC == 1 ? PNTF_NO1 : 1; }
 
-// Generic layer: out tiles processed NO at a time (NO*NC >= 2 independent MFMA chains).
-//   init(ot, acc[o][c])  before the K loop of out-tile group starting at ot
-//   epi(ot, acc)         after it
-template <int OT, int KT, int NC, int SITE, int NIN, class InitF, class EpiF>
-__device__ __forceinline__ void layer(Rsrc W, int wbase, const f32x4 (&in)[NIN], int lane,
-                                      InitF init, EpiF epi) {
+// "No previous layer tail" hook.
+struct NoPre {
+  template <class ST>
+  __device__ void operator()(ST) const {}
+};
+
+// ---------------------------------------------------------------- generic layer
+// Epilogue units per out tile: a tile's epilogue runs as EP_SPLIT units of 4/EP_SPLIT rows,
+// one unit per step, so no step carries more VALU work than its MFMAs can shadow.
+#ifndef PNTF_EP_SPLIT
+#define PNTF_EP_SPLIT 2
+#endif
+constexpr int EP_SPLIT = PNTF_EP_SPLIT;
+constexpr int EP_ROWS = 4 / EP_SPLIT;
+
+// One Linear layer as out-tile groups of NO tiles x NC columns (NO*NC >= 2 independent MFMA
+// chains); a step consumes KS k-tiles (NO*KS weight fragments), KT/KS steps per group.  The
+// layer object ly supplies
+//   ly.init(ot, acc)      at the first step of the group starting at out tile ot
+//   ly.epi(t, c, h, v)    unit h (rows h*EP_ROWS ..) of the epilogue of out tile t, column c,
+//                         from v[NC] = that tile's accumulators; runs deferred, one unit per
+//                         step in the first NO*NC*EP_SPLIT steps of the next group
+//   ly.pend[NO][NC]       holds the last group's accumulators on return: its epilogue is
+//                         still pending (run it with flush(), or as the next layer's pre hook)
+// pre(st) runs at every step (the previous layer's pending tail; a no-op past its length).
+template <int OT, int KT, int NC, int KS, int SITE, int NLN, int NIN, class L, class PreF,
+          class NextF>
+__device__ __forceinline__ void layer(Ring& ring, Rsrc W, int wbase, const f32x4 (&in)[NIN],
+                                      int lane, L& ly, PreF pre, NextF naddr) {
   constexpr int NO = out_group<NC>();
-  constexpr int STEPS = (OT / NO) * KT;
+  constexpr int GS = KT / KS;                 // steps per group
+  constexpr int STEPS = (OT / NO) * GS;
+  constexpr int UNITS = NO * NC * EP_SPLIT;   // deferred epilogue units per group
+  static_assert(KT % KS == 0 && UNITS <= GS, "a group's epilogue must fit in the next group");
   f32x4 acc[NO][NC];
-  pipelined<STEPS, NO, PF_STEPS, SITE>(
-      W, lane * 16,
-      [&](int st, int l) { return frag<KT>(wbase, (st / KT) * NO + l, st % KT); },
-      [&](auto st, const f32x4 (&a)[NO]) {
-        constexpr int ot = (decltype(st)::value / KT) * NO, kt = decltype(st)::value % KT;
-        if constexpr (kt == 0) init(ot, acc);
+  run_steps<STEPS, NO * KS, NLN, SITE>(
+      ring, W, lane * 16,
+      [&](int st, int l) {
+        return frag<KT>(wbase, (st / GS) * NO + l / KS, (st % GS) * KS + l % KS);
+      },
+      naddr,
+      [&](auto st, const f32x4 (&a)[NO * KS]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int ot = (S / GS) * NO, ks0 = (S % GS) * KS;
+        pre(st);
+        if constexpr (S % GS == 0) ly.init(ot, acc);
+        if constexpr (ot > 0 && S % GS < UNITS) {
+          constexpr int u = S % GS;
+          ly.epi(ot - NO + u / (NC * EP_SPLIT), (u / EP_SPLIT) % NC, u % EP_SPLIT,
+                 ly.pend[u / (NC * EP_SPLIT)]);
+        }
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int o = 0; o < NO; ++o)
+#pragma unroll
+              for (int c = 0; c < NC; ++c)
+                acc[o][c] = mfma(a[o * KS + k][s], in[c * KT + ks0 + k][s], acc[o][c]);
+        if constexpr (S % GS == GS - 1) {
 #pragma unroll
           for (int o = 0; o < NO; ++o)
 #pragma unroll
-            for (int c = 0; c < NC; ++c) acc[o][c] = mfma(a[o][s], in[c * KT + kt][s], acc[o][c]);
-        if constexpr (kt == KT - 1) epi(ot, acc);
-      });
-}
-
-// ---------------------------------------------------------------- forward layers
-// out[c*OT+ot] = softplus(A·in + bias (+ out[c*OT+ot] if RES)); σ10(pre) saved to scratch
-// tile sc0 + c*OT + ot when SAVE.
-template <int OT, int KT, int NC, bool RES, bool SAVE>
-__device__ __forceinline__ void fwd_act_layer(Rsrc W, int wbase, int bias,
-                                              const f32x4 (&in)[16], f32x4 (&out)[16],
-                                              Scratch sc, int sc0, int lane) {
-  constexpr int NO = out_group<NC>();
-  const int g = lane >> 4;
-  layer<OT, KT, NC, NC == 2 ? SITE_FWD_ENC : SITE_FWD_GEN>(
-      W, wbase, in, lane,
-      [&](int ot, f32x4 (&acc)[NO][NC]) {
-#pragma unroll
-        for (int o = 0; o < NO; ++o) {
-          f32x4 b = bload(W, g * 16, bias + (16 * (ot + o)) * 4);
-#pragma unroll
-          for (int c = 0; c < NC; ++c) acc[o][c] = RES ? out[c * OT + ot + o] + b : b;
+            for (int c = 0; c < NC; ++c) ly.pend[o][c] = acc[o][c];
         }
-      },
-      [&](int ot, f32x4 (&acc)[NO][NC]) {
-#pragma unroll
-        for (int o = 0; o < NO; ++o)
-#pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            f32x4 s, sg;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              SpSig v = sp_sig(acc[o][c][r]);
-              s[r] = v.sp;
-              sg[r] = v.sg;
-            }
-            out[c * OT + ot + o] = s;
-            if (SAVE) store_tile(sc, sc0 + c * OT + ot + o, lane, sg);
-          }
       });
 }
 
-// out[c*OT+ot] = A·in + bias, no activation (encoder[-1], :234).
-template <int OT, int KT, int NC>
-__device__ __forceinline__ void fwd_lin_layer(Rsrc W, int wbase, int bias,
-                                              const f32x4 (&in)[16], f32x4 (&out)[16],
-                                              int lane) {
-  constexpr int NO = out_group<NC>();
-  const int g = lane >> 4;
-  layer<OT, KT, NC, NC == 2 ? SITE_FWD_ENC : SITE_FWD_GEN>(
-      W, wbase, in, lane,
-      [&](int ot, f32x4 (&acc)[NO][NC]) {
-#pragma unroll
-        for (int o = 0; o < NO; ++o) {
-          f32x4 b = bload(W, g * 16, bias + (16 * (ot + o)) * 4);
-#pragma unroll
-          for (int c = 0; c < NC; ++c) acc[o][c] = b;
-        }
-      },
-      [&](int ot, f32x4 (&acc)[NO][NC]) {
-#pragma unroll
-        for (int o = 0; o < NO; ++o)
-#pragma unroll
-          for (int c = 0; c < NC; ++c) out[c * OT + ot + o] = acc[o][c];
-      });
+// The pending epilogue of a layer's last group as a pre hook for the next layer (unit j at
+// its step j; safe while that layer reads the pending tiles only at those or later steps) ...
+template <class L>
+struct Tail {
+  L& ly;
+  template <class ST>
+  __device__ __forceinline__ void operator()(ST) const {
+    constexpr int j = ST::value;
+    if constexpr (j < L::NO * L::NC * EP_SPLIT)
+      ly.epi(L::OT - L::NO + j / (L::NC * EP_SPLIT), (j / EP_SPLIT) % L::NC, j % EP_SPLIT,
+             ly.pend[j / (L::NC * EP_SPLIT)]);
+  }
+};
+// ... or run at once.
+template <class L>
+__device__ __forceinline__ void flush(L& ly) {
+  Tail<L> t{ly};
+  static_for<0, L::NO * L::NC * EP_SPLIT>([&](auto j) { t(j); });
 }
 
-// ---------------------------------------------------------------- backward layers
-// out[c*OT+ot] = (A^T·in (+ out[c*OT+ot] if RES)) ⊙ scratch[mul0 + c*OT + ot] (if MUL)
-template <int OT, int KT, int NC, bool RES, bool MUL>
-__device__ __forceinline__ void bwd_layer(Rsrc W, int wbase, const f32x4 (&in)[16],
-                                          f32x4 (&out)[16], Scratch sc,
-                                          int mul0, int lane) {
-  constexpr int NO = out_group<NC>();
-  f32x4 m[NO][NC];
-  layer<OT, KT, NC, NC == 2 ? SITE_BWD_ENC : SITE_BWD_GEN>(
-      W, wbase, in, lane,
-      [&](int ot, f32x4 (&acc)[NO][NC]) {
+// ---------------------------------------------------------------- layer kinds
+// Forward: out[c*OT+t] = softplus(A·in + bias (+ out[c*OT+t] if RES)); σ10(pre) saved to
+// scratch tile sc0 + c*OT + t when SAVE, and kept in keep[t] when KEEP (single column).
+template <int OT_, int KT_, int NC_, bool RES, bool SAVE, bool KEEP = false>
+struct FwdAct {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_>();
+  Rsrc W;
+  int bias;
+  f32x4 (&out)[16];
+  Scratch sc;
+  int sc0, lane;
+  f32x4 (&keep)[8];
+  f32x4 bb[2][NO];
+  f32x4 pend[NO][NC];
+  __device__ __forceinline__ void init(int ot, f32x4 (&acc)[NO][NC]) {
+    const int par = (ot / NO) & 1;
 #pragma unroll
-        for (int o = 0; o < NO; ++o)
+    for (int o = 0; o < NO; ++o) {
+      bb[par][o] = bload(W, (lane >> 4) * 16, bias + (16 * (ot + o)) * 4);
 #pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            if (MUL) m[o][c] = load_tile(sc, mul0 + c * OT + ot + o, lane);
-            acc[o][c] = RES ? out[c * OT + ot + o] : f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-      },
-      [&](int ot, f32x4 (&acc)[NO][NC]) {
+      for (int c = 0; c < NC; ++c) acc[o][c] = RES ? out[c * OT + ot + o] : zero4();
+    }
+  }
+  f32x4 sgp;   // σ rows of the tile being finished (units of one tile are consecutive)
+  __device__ __forceinline__ void epi(int t, int c, int h, const f32x4 (&v)[NC]) {
+    const f32x4 b = bb[(t / NO) & 1][t % NO];
 #pragma unroll
-        for (int o = 0; o < NO; ++o)
+    for (int r = h * EP_ROWS; r < (h + 1) * EP_ROWS; ++r) {
+      SpSig q = sp_sig(v[c][r] + b[r]);
+      out[c * OT + t][r] = q.sp;
+      sgp[r] = q.sg;
+    }
+    if (h == EP_SPLIT - 1) {
+      if (SAVE) store_tile(sc, sc0 + c * OT + t, lane, sgp);
+      if (KEEP) keep[t] = sgp;
+    }
+  }
+};
+
+// out[c*OT+t] = A·in + bias, no activation (encoder[-1], :234).
+template <int OT_, int KT_, int NC_>
+struct FwdLin {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_>();
+  Rsrc W;
+  int bias;
+  f32x4 (&out)[16];
+  int lane;
+  f32x4 bb[2][NO];
+  f32x4 pend[NO][NC];
+  __device__ __forceinline__ void init(int ot, f32x4 (&acc)[NO][NC]) {
+    const int par = (ot / NO) & 1;
 #pragma unroll
-          for (int c = 0; c < NC; ++c)
-            out[c * OT + ot + o] = MUL ? acc[o][c] * m[o][c] : acc[o][c];
-      });
-}
+    for (int o = 0; o < NO; ++o) {
+      bb[par][o] = bload(W, (lane >> 4) * 16, bias + (16 * (ot + o)) * 4);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[o][c] = zero4();
+    }
+  }
+  __device__ __forceinline__ void epi(int t, int c, int h, const f32x4 (&v)[NC]) {
+    const f32x4 b = bb[(t / NO) & 1][t % NO];
+#pragma unroll
+    for (int r = h * EP_ROWS; r < (h + 1) * EP_ROWS; ++r) out[c * OT + t][r] = v[c][r] + b[r];
+  }
+};
+
+// Reverse: out[c*OT+t] = (A^T·in (+ out[c*OT+t] if RES)) ⊙ scratch[mul0 + c*OT + t] (if MUL)
+template <int OT_, int KT_, int NC_, bool RES, bool MUL>
+struct Bwd {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_>();
+  f32x4 (&out)[16];
+  Scratch sc;
+  int mul0, lane;
+  f32x4 m[2][NO][NC];
+  f32x4 pend[NO][NC];
+  __device__ __forceinline__ void init(int ot, f32x4 (&acc)[NO][NC]) {
+    const int par = (ot / NO) & 1;
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (MUL) m[par][o][c] = load_tile(sc, mul0 + c * OT + ot + o, lane);
+        acc[o][c] = RES ? out[c * OT + ot + o] : zero4();
+      }
+  }
+  __device__ __forceinline__ void epi(int t, int c, int h, const f32x4 (&v)[NC]) {
+    const f32x4 mm = m[(t / NO) & 1][t % NO][c];
+#pragma unroll
+    for (int r = h * EP_ROWS; r < (h + 1) * EP_ROWS; ++r)
+      out[c * OT + t][r] = MUL ? v[c][r] * mm[r] : v[c][r];
+  }
+};
 
 // ---------------------------------------------------------------- one pair tile
 struct PairIO {
   float x[2][6];    // [start|goal][dim]
   const float* Bw;  // this lane's env B (dim x 128), un-scaled
+};
+
+// Registers a pair tile carries from the forward pass into the reverse sweep.
+struct Carry {
+  f32x4 sg3[8];   // σ10 of generator[-2] (:251-252)
+  f32x4 g4w[8];   // generator[-1].weight rows of this lane
 };
 
 // q = x · (2π B) for the lane's 4 feature rows of Fourier tile kt, both columns.
@@ -334,12 +486,31 @@ __device__ __forceinline__ void fourier_tile(const PairIO& io, int kt, int g, f3
     }
 }
 
-// Forward pass (NN.out).  GRAD: also save σ tiles for the reverse sweep.
+// Ring head of the forward pass (encoder[0] on Fourier features): step j reads fragments
+// (out tile j % 8, k tile j / 8 + 8 l).
+struct E0Head {
+  __device__ int operator()(int j, int l) const {
+    return frag<16>((OFF_FWD + OFF_E0) * 4, j % 8, j / 8 + 8 * l);
+  }
+};
+// Ring head of the reverse sweep (generator[-2]^T, 256 x 128: OT 16, KT 8).
+__device__ __forceinline__ Head<8> bwd_head() { return Head<8>{(OFF_BWD + OFF_G3) * 4}; }
+// Ring head of the Fourier fold (encoder[0]^T, 256 x 128: KT 8): fragments (kf, kt) and
+// (kf + 8, kt) for step (kf, kt).
+struct FoldHead {
+  __device__ int operator()(int j, int l) const {
+    return frag<8>((OFF_BWD + OFF_E0) * 4, j / 8 + 8 * l, j % 8);
+  }
+};
+
+// Forward pass (NN.out).  GRAD: also save σ tiles for the reverse sweep.  On entry the ring
+// holds E0Head; on return it holds the first PF steps of `after` (NLA fragments per step).
 // Returns τ for the lane's pair (identical in all four lane groups).
-template <int DIM, bool GRAD>
-__device__ __forceinline__ float forward_pass(const float* __restrict__ P, const PairIO& io,
-                                              f32x4 (&X)[16], f32x4 (&Y)[16],
-                                              Scratch sc, int compat, int lane) {
+template <int DIM, bool GRAD, int NLA, class AfterF>
+__device__ __forceinline__ float forward_pass(Ring& ring, const float* __restrict__ P,
+                                              const PairIO& io, f32x4 (&X)[16], f32x4 (&Y)[16],
+                                              Carry& cy, Scratch sc, int compat, int lane,
+                                              AfterF after) {
   const int g = lane >> 4;
   const Rsrc W = make_rsrc(P, PACKED_FLOATS * 4);
   constexpr int BB = OFF_BIAS * 4;  // byte base of biases / head
@@ -349,69 +520,104 @@ __device__ __forceinline__ float forward_pass(const float* __restrict__ P, const
 
   // ---- encoder[0] on Fourier features computed on the fly (:186-190, :227).
   // E0 is (128 x 256): OT = 8, KT = 16; input tiles 0..7 = sin q, 8..15 = cos q.
-  // Step (kt, ot) loads fragments (ot, kt) and (ot, kt + 8).
+  // Step (kt, ot) uses fragments (ot, kt) and (ot, kt + 8); out tile ot is complete after
+  // step (7, ot), and its epilogue runs in step (7, ot + 1) (tile 7's in the next layer).
+  PNTF_STAMP(0);
+  f32x4 eb[8];
+  // encoder[0] epilogue of out tile i (columns 0, 1): bias, softplus, σ; in compat mode the
+  // out_backgrad quirk (:435-438) stores σ10(softplus(y)) = 1 / (2 - σ10(y)).
+  auto e0epi = [&](int i) {
 #pragma unroll
-  for (int ot = 0; ot < 8; ++ot) {
-    f32x4 b = bload(W, g * 16, BB + (B_E0 + 16 * ot) * 4);
-    X[ot] = b;
-    X[8 + ot] = b;
-  }
+    for (int c = 0; c < 2; ++c) {
+      const int t = c * 8 + i;
+      f32x4 s, sg;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        SpSig v = sp_sig(X[t][r] + eb[i][r]);
+        s[r] = v.sp;
+        sg[r] = fmaf(cm, __builtin_amdgcn_rcpf(2.f - v.sg) - v.sg, v.sg);
+      }
+      X[t] = s;
+      if (GRAD) store_tile(sc, T_E0 + t, lane, sg);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < 16; ++i) X[i] = zero4();
   {
     f32x4 sn[2], cs[2];
-    pipelined<64, 2, PF_STEPS, SITE_FWD_E0>(
-        W, lane * 16,
+    f32x4 bw[2][DIM];   // B rows of the lane's features, one Fourier tile ahead
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) bw[0][d] = ld4(io.Bw + d * H + 4 * g);
+    run_steps<64, 2, 2, SITE_FWD_E0>(
+        ring, W, lane * 16,
         [&](int st, int l) { return frag<16>(F + OFF_E0 * 4, st % 8, st / 8 + 8 * l); },
+        Head<8, 2>{F + OFF_EBLK * 4},
         [&](auto st, const f32x4 (&a)[2]) {
-          constexpr int kt = decltype(st)::value / 8, ot = decltype(st)::value % 8;
+          constexpr int S = decltype(st)::value;
+          constexpr int kt = S / 8, ot = S % 8;
+          if constexpr (S == 1) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) eb[t] = bload(W, g * 16, BB + (B_E0 + 16 * t) * 4);
+          }
+          if constexpr (ot == 1 && kt < 7) {
+#pragma unroll
+            for (int d = 0; d < DIM; ++d) bw[(kt + 1) & 1][d] = ld4(io.Bw + d * H + 16 * (kt + 1) + 4 * g);
+          }
           if constexpr (ot == 0) {
-            f32x4 w[DIM], q[2];
-            fourier_tile<DIM>(io, kt, g, w, q);
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll
               for (int s = 0; s < 4; ++s) {
+                float q = 0.f;
+#pragma unroll
+                for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], TWO_PI * bw[kt & 1][d][s], q);
                 float x0, x1;
-                sincos_fast(q[c][s], x0, x1);
+                sincos_fast(q, x0, x1);
                 sn[c][s] = x0;
                 cs[c][s] = x1;
               }
           }
+          if constexpr (kt == 7 && ot > 0) e0epi(ot - 1);
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
+          for (int s = 0; s < 4; ++s) {
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              X[c * 8 + ot] = mfma(a[0][s], sn[c][s], X[c * 8 + ot]);
-              X[c * 8 + ot] = mfma(a[1][s], cs[c][s], X[c * 8 + ot]);
-            }
+            for (int c = 0; c < 2; ++c) X[c * 8 + ot] = mfma(a[0][s], sn[c][s], X[c * 8 + ot]);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) X[c * 8 + ot] = mfma(a[1][s], cs[c][s], X[c * 8 + ot]);
+          }
         });
   }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    f32x4 s, sg;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      SpSig v = sp_sig(X[i][r]);
-      s[r] = v.sp;
-      sg[r] = cm * sig10(v.sp) + (1.f - cm) * v.sg;   // out_backgrad quirk (:435-438)
-    }
-    X[i] = s;
-    if (GRAD) store_tile(sc, T_E0 + i, lane, sg);
-    PNTF_DBG(i, sg);
-    PNTF_DBG(16 + i, s);
-  }
+  PNTF_STAMP(1);
 
-  // ---- encoder residual blocks (:228-232); X = h (2 cols x 8 tiles)
-#pragma unroll 1
-  for (int b = 0; b < 2; ++b) {
-    const int wa = opaque(F + (OFF_EBLK + (2 * b) * SZ_E) * 4);
-    const int wb = opaque(F + (OFF_EBLK + (2 * b + 1) * SZ_E) * 4);
-    fwd_act_layer<8, 8, 2, false, GRAD>(W, wa, BB + (B_EBLK + (2 * b) * 128) * 4, X, Y, sc,
-                                        T_EBLK + 32 * b, lane);
-    fwd_act_layer<8, 8, 2, true, GRAD>(W, wb, BB + (B_EBLK + (2 * b + 1) * 128) * 4, Y, X, sc,
-                                       T_EBLK + 32 * b + 16, lane);
-  }
+  // ---- encoder residual blocks (:228-232), unrolled; X = h (2 cols x 8 tiles)
+  const int BE = BB + B_EBLK * 4;
+  const int WE = F + OFF_EBLK * 4;
+  FwdAct<8, 8, 2, false, GRAD> a0{W, BE, Y, sc, T_EBLK, lane, cy.sg3};
+  layer<8, 8, 2, 2, SITE_FWD_ENC, 2>(
+      ring, W, WE, X, lane, a0,
+      [&](auto st) {
+        if constexpr (decltype(st)::value == 0) e0epi(7);
+      },
+      Head<8, 2>{WE + SZ_E * 4});
+  PNTF_STAMP(2);
+  FwdAct<8, 8, 2, true, GRAD> b0{W, BE + 128 * 4, X, sc, T_EBLK + 16, lane, cy.sg3};
+  layer<8, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + SZ_E * 4, Y, lane, b0, Tail<decltype(a0)>{a0},
+                                  Head<8, 2>{WE + 2 * SZ_E * 4});
+  PNTF_STAMP(3);
+  FwdAct<8, 8, 2, false, GRAD> a1{W, BE + 256 * 4, Y, sc, T_EBLK + 32, lane, cy.sg3};
+  layer<8, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
+                                  Tail<decltype(b0)>{b0}, Head<8, 2>{WE + 3 * SZ_E * 4});
+  PNTF_STAMP(4);
+  FwdAct<8, 8, 2, true, GRAD> b1{W, BE + 384 * 4, X, sc, T_EBLK + 48, lane, cy.sg3};
+  layer<8, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
+                                  Tail<decltype(a1)>{a1}, Head<8, 2>{F + OFF_E3 * 4});
+  PNTF_STAMP(5);
   // ---- encoder[-1] (:234) -> Y (zs = Y[0..7], zg = Y[8..15])
-  fwd_lin_layer<8, 8, 2>(W, F + OFF_E3 * 4, BB + B_E3 * 4, X, Y, lane);
+  FwdLin<8, 8, 2> e3{W, BB + B_E3 * 4, Y, lane};
+  layer<8, 8, 2, 2, SITE_FWD_ENC, 4>(ring, W, F + OFF_E3 * 4, X, lane, e3, Tail<decltype(b1)>{b1},
+                                  Head<16>{F + OFF_GBLK * 4});
+  flush(e3);
+  PNTF_STAMP(6);
 
   // ---- symmetric smooth max / min merge (:236-244) -> X (u = [M | m], 16 tiles)
 #pragma unroll
@@ -430,53 +636,79 @@ __device__ __forceinline__ float forward_pass(const float* __restrict__ P, const
     }
     if (GRAD) store_tile(sc, T_S0 + t, lane, s0);
   }
+  PNTF_STAMP(7);
 
   // ---- generator residual blocks (:246-249); X = u (16 tiles)
 #pragma unroll 1
   for (int i = 0; i < 3; ++i) {
     const int wa = opaque(F + (OFF_GBLK + (2 * i) * SZ_G) * 4);
     const int wb = opaque(F + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4);
-    fwd_act_layer<16, 16, 1, false, GRAD>(W, wa, BB + (B_GBLK + (2 * i) * 256) * 4, X, Y, sc,
-                                          T_GBLK + 32 * i, lane);
-    fwd_act_layer<16, 16, 1, true, GRAD>(W, wb, BB + (B_GBLK + (2 * i + 1) * 256) * 4, Y, X, sc,
-                                         T_GBLK + 32 * i + 16, lane);
+    const int wn = opaque(i < 2 ? F + (OFF_GBLK + (2 * i + 2) * SZ_G) * 4 : F + OFF_G3 * 4);
+    FwdAct<16, 16, 1, false, GRAD> ga{W, BB + (B_GBLK + (2 * i) * 256) * 4, Y, sc,
+                                      T_GBLK + 32 * i, lane, cy.sg3};
+    layer<16, 16, 1, 1, SITE_FWD_GEN, 4>(ring, W, wa, X, lane, ga, NoPre{}, Head<16>{wb});
+    FwdAct<16, 16, 1, true, GRAD> gb{W, BB + (B_GBLK + (2 * i + 1) * 256) * 4, X, sc,
+                                     T_GBLK + 32 * i + 16, lane, cy.sg3};
+    layer<16, 16, 1, 1, SITE_FWD_GEN, 4>(ring, W, wb, Y, lane, gb, Tail<decltype(ga)>{ga},
+                                      Head<16>{wn});
+    flush(gb);
   }
-  // ---- generator[-2] + act (:251-252) -> Y[0..7]
-  fwd_act_layer<8, 16, 1, false, GRAD>(W, F + OFF_G3 * 4, BB + B_G3 * 4, X, Y, sc, T_G3, lane);
+  PNTF_STAMP(13);
+  // ---- generator[-2] + act (:251-252) -> Y[0..7]; its σ tiles stay in registers for the
+  // reverse sweep, and the head row is fetched while it runs.
+#pragma unroll
+  for (int t = 0; t < 8; ++t) cy.g4w[t] = bload(W, g * 16, BB + (B_G4W + 16 * t) * 4);
+  const float g4b = bload(W, 0, BB + B_G4B * 4)[0];
+  FwdAct<8, 16, 1, false, GRAD, GRAD> g3{W, BB + B_G3 * 4, Y, sc, T_G3, lane, cy.sg3};
+  layer<8, 16, 1, 1, SITE_FWD_GEN, NLA>(ring, W, F + OFF_G3 * 4, X, lane, g3, NoPre{}, after);
+  flush(g3);
+  PNTF_STAMP(14);
 
   // ---- head generator[-1] + sigmoid(0.1 y) (:254-255)
   float part = 0.f;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    f32x4 g4 = bload(W, g * 16, BB + (B_G4W + 16 * t) * 4);
+  for (int t = 0; t < 8; ++t)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) part = fmaf(g4[s], Y[t][s], part);
-  }
+    for (int s = 0; s < 4; ++s) part = fmaf(cy.g4w[t][s], Y[t][s], part);
   part += __shfl_xor(part, 16);
   part += __shfl_xor(part, 32);
-  float y4 = part + bload(W, 0, BB + B_G4B * 4)[0];
+  float y4 = part + g4b;
+  PNTF_STAMP(15);
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-0.144269504088896341f * y4));
 }
 
 // Reverse sweep: exact reverse mode, or NN.out_backgrad when the forward stored the quirk.
-// Produces dτ/dxs (ds) and dτ/dxg (dg), identical in all four lane groups.
-template <int DIM>
-__device__ __forceinline__ void backward_pass(const float* __restrict__ P, const PairIO& io,
-                                              float tau, f32x4 (&X)[16], f32x4 (&Y)[16],
-                                              Scratch sc, int lane,
-                                              float (&ds)[DIM], float (&dg)[DIM]) {
+// On entry the ring holds bwd_head(); on return the first PF steps of `after`.  Produces
+// dτ/dxs (ds) and dτ/dxg (dg), identical in all four lane groups.
+template <int DIM, int NLA, class AfterF>
+__device__ __forceinline__ void backward_pass(Ring& ring, const float* __restrict__ P,
+                                              const PairIO& io, float tau, f32x4 (&X)[16],
+                                              f32x4 (&Y)[16], const Carry& cy, Scratch sc,
+                                              int lane, float (&ds)[DIM], float (&dg)[DIM],
+                                              AfterF after) {
   const int g = lane >> 4;
   const Rsrc W = make_rsrc(P, PACKED_FLOATS * 4);
-  constexpr int BB = OFF_BIAS * 4;  // byte base of biases / head
   constexpr int Bk = OFF_BWD * 4;  // byte base of the transposed fragments
 
   // ---- head and generator[-2] (:592-613): Y[t] = d * G4 ⊙ σ10(y3)
   const float dd = 0.1f * tau * (1.f - tau);
 #pragma unroll
-  for (int t = 0; t < 8; ++t)
-    Y[t] = (dd * bload(W, g * 16, BB + (B_G4W + 16 * t) * 4)) * load_tile(sc, T_G3 + t, lane);
+  for (int t = 0; t < 8; ++t) Y[t] = (dd * cy.g4w[t]) * cy.sg3[t];
+  PNTF_STAMP(17);
   // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> X  (G3^T is 256 x 128: OT 16, KT 8)
-  bwd_layer<16, 8, 1, false, true>(W, Bk + OFF_G3 * 4, Y, X, sc, T_GBLK + 32 * 2 + 16, lane);
+  {
+    Bwd<16, 8, 1, false, true> l{X, sc, T_GBLK + 32 * 2 + 16, lane};
+    layer<16, 8, 1, 1, SITE_BWD_GEN, 4>(ring, W, Bk + OFF_G3 * 4, Y, lane, l, NoPre{},
+                                     Head<16>{Bk + (OFF_GBLK + 5 * SZ_G) * 4});
+    flush(l);
+  }
+  PNTF_STAMP(18);
+#ifdef PNTF_S0_EARLY
+  // the merge switch tiles, fetched now and held through the generator sweep
+  f32x4 s0t[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) s0t[t] = load_tile(sc, T_S0 + t, lane);
+#endif
 
   // ---- generator blocks, reverse (:615-618)
 #pragma unroll 1
@@ -484,88 +716,125 @@ __device__ __forceinline__ void backward_pass(const float* __restrict__ P, const
     const int wa = opaque(Bk + (OFF_GBLK + (2 * i) * SZ_G) * 4);
     const int wb = opaque(Bk + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4);
     // da = (G1_i^T dr) ⊙ σ10(y1_i) -> Y
-    bwd_layer<16, 16, 1, false, true>(W, wb, X, Y, sc, T_GBLK + 32 * i, lane);
+    Bwd<16, 16, 1, false, true> lb{Y, sc, T_GBLK + 32 * i, lane};
+    layer<16, 16, 1, 1, SITE_BWD_GEN, 4>(ring, W, wb, X, lane, lb, NoPre{}, Head<16>{wa});
     // du = G_i^T da + dr, then ⊙ σ10(y2_{i-1}) for the next block (none after block 0)
-    if (i > 0)
-      bwd_layer<16, 16, 1, true, true>(W, wa, Y, X, sc, T_GBLK + 32 * (i - 1) + 16, lane);
-    else
-      bwd_layer<16, 16, 1, true, false>(W, wa, Y, X, sc, 0, lane);
+    if (i > 0) {
+      const int wn = opaque(Bk + (OFF_GBLK + (2 * i - 1) * SZ_G) * 4);
+      Bwd<16, 16, 1, true, true> la{X, sc, T_GBLK + 32 * (i - 1) + 16, lane};
+      layer<16, 16, 1, 1, SITE_BWD_GEN, 4>(ring, W, wa, Y, lane, la, Tail<decltype(lb)>{lb},
+                                        Head<16>{wn});
+      flush(la);
+    } else {
+      Bwd<16, 16, 1, true, false> la{X, sc, 0, lane};
+      layer<16, 16, 1, 1, SITE_BWD_GEN, 2>(ring, W, wa, Y, lane, la, Tail<decltype(lb)>{lb},
+                                        Head<8, 2>{Bk + OFF_E3 * 4});
+      flush(la);
+    }
   }
+  PNTF_STAMP(24);
 
   // ---- merge Jacobian (:620-627): X[0..7] = dzs, X[8..15] = dzg
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
+#ifdef PNTF_S0_EARLY
+    f32x4 s0 = s0t[t];
+#else
     f32x4 s0 = load_tile(sc, T_S0 + t, lane);
+#endif
     f32x4 s1 = 1.f - s0;
     f32x4 dM = X[t], dm = X[8 + t];
     X[t] = s0 * dM + s1 * dm;
     X[8 + t] = s1 * dM + s0 * dm;
   }
+  PNTF_STAMP(25);
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1) -> Y
-  bwd_layer<8, 8, 2, false, true>(W, Bk + OFF_E3 * 4, X, Y, sc, T_EBLK + 32 * 1 + 16, lane);
-  // ---- encoder blocks, reverse (:633-636)
-#pragma unroll 1
-  for (int b = 1; b >= 0; --b) {
-    const int wa = opaque(Bk + (OFF_EBLK + (2 * b) * SZ_E) * 4);
-    const int wb = opaque(Bk + (OFF_EBLK + (2 * b + 1) * SZ_E) * 4);
-    bwd_layer<8, 8, 2, false, true>(W, wb, Y, X, sc, T_EBLK + 32 * b, lane);
-    // dh = E_i^T da + dr, then ⊙ σ10 of the layer below (block 0's y2, or encoder[0])
-    bwd_layer<8, 8, 2, true, true>(W, wa, X, Y, sc, b > 0 ? T_EBLK + 16 : T_E0, lane);
-  }
+  const int WE = Bk + OFF_EBLK * 4;
+  Bwd<8, 8, 2, false, true> e3{Y, sc, T_EBLK + 32 * 1 + 16, lane};
+  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, Bk + OFF_E3 * 4, X, lane, e3, NoPre{},
+                                  Head<8, 2>{WE + 3 * SZ_E * 4});
+  PNTF_STAMP(26);
+  // ---- encoder blocks, reverse (:633-636), unrolled
+  // da = (E1_b^T dr) ⊙ σ10(y1_b)
+  Bwd<8, 8, 2, false, true> b1{X, sc, T_EBLK + 32, lane};
+  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
+                                  Tail<decltype(e3)>{e3}, Head<8, 2>{WE + 2 * SZ_E * 4});
+  PNTF_STAMP(27);
+  // dh = E_b^T da + dr, then ⊙ σ10 of the layer below (block 0's y2, or encoder[0])
+  Bwd<8, 8, 2, true, true> a1{Y, sc, T_EBLK + 16, lane};
+  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
+                                  Tail<decltype(b1)>{b1}, Head<8, 2>{WE + 1 * SZ_E * 4});
+  PNTF_STAMP(28);
+  Bwd<8, 8, 2, false, true> b0{X, sc, T_EBLK, lane};
+  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0,
+                                  Tail<decltype(a1)>{a1}, Head<8, 2>{WE});
+  PNTF_STAMP(29);
+  Bwd<8, 8, 2, true, true> a0{Y, sc, T_E0, lane};
+  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE, X, lane, a0, Tail<decltype(b0)>{b0}, FoldHead{});
+  PNTF_STAMP(30);
 
   // ---- encoder[0]^T (256 x 128: OT 16, KT 8) fused with the Fourier Jacobian (:639-645)
-  // Step (kf, kt) loads fragments (kf, kt) [dφ_sin rows] and (kf + 8, kt) [dφ_cos rows].
+  // Step (kf, kt) uses fragments (kf, kt) [dφ_sin rows] and (kf + 8, kt) [dφ_cos rows].  The
+  // Fourier fold of feature tile kf runs deferred in the first steps of feature tile kf + 1.
   float acc[2][DIM];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) PNTF_DBG(32 + i, Y[i]);
-#pragma unroll
   for (int d = 0; d < DIM; ++d) acc[0][d] = acc[1][d] = 0.f;
-  f32x4 ph[2][2];
-  pipelined<64, 2, PF_STEPS, SITE_FOLD>(
-      W, lane * 16,
-      [&](int st, int l) { return frag<8>(Bk + OFF_E0 * 4, st / 8 + 8 * l, st % 8); },
+  f32x4 ph[2][2][2];   // [kf parity][sin|cos rows][column]
+  f32x4 bw[2][DIM];    // B rows of the lane's features of tile kf (fetched in step (kf, 2))
+  auto fold = [&](int kf, int c) {
+    const int p = kf & 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float q = 0.f;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], TWO_PI * bw[p][d][s], q);
+      float sn, cs;
+      sincos_fast(q, sn, cs);
+      float gg = ph[p][0][c][s] * cs - ph[p][1][c][s] * sn;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) acc[c][d] = fmaf(TWO_PI * bw[p][d][s], gg, acc[c][d]);
+    }
+  };
+  Tail<decltype(a0)> a0tail{a0};
+  run_steps<64, 2, NLA, SITE_FOLD>(
+      ring, W, lane * 16,
+      [&](int st, int l) { return frag<8>(Bk + OFF_E0 * 4, st / 8 + 8 * l, st % 8); }, after,
       [&](auto st, const f32x4 (&a)[2]) {
-        constexpr int kf = decltype(st)::value / 8, kt = decltype(st)::value % 8;
+        constexpr int S = decltype(st)::value;
+        constexpr int kf = S / 8, kt = S % 8, p = kf & 1;
+        a0tail(st);
         if constexpr (kt == 0) {
 #pragma unroll
           for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int c = 0; c < 2; ++c) ph[u][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < 2; ++c) ph[p][u][c] = zero4();
         }
+        if constexpr (kt == 2) {
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) bw[p][d] = ld4(io.Bw + d * H + 16 * kf + 4 * g);
+        }
+        if constexpr (kf > 0 && kt < 2) fold(kf - 1, kt);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
-            ph[0][c] = mfma(a[0][s], Y[c * 8 + kt][s], ph[0][c]);
-            ph[1][c] = mfma(a[1][s], Y[c * 8 + kt][s], ph[1][c]);
+            ph[p][0][c] = mfma(a[0][s], Y[c * 8 + kt][s], ph[p][0][c]);
+            ph[p][1][c] = mfma(a[1][s], Y[c * 8 + kt][s], ph[p][1][c]);
           }
-        if constexpr (kt == 7) {
-          f32x4 w[DIM], q[2];
-          fourier_tile<DIM>(io, kf, g, w, q);
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              float sn, cs;
-              sincos_fast(q[c][s], sn, cs);
-              float gg = ph[0][c][s] * cs - ph[1][c][s] * sn;
-#pragma unroll
-              for (int d = 0; d < DIM; ++d) acc[c][d] = fmaf(w[d][s], gg, acc[c][d]);
-            }
-        }
       });
+  fold(7, 0);
+  fold(7, 1);
 #pragma unroll
   for (int d = 0; d < DIM; ++d) {
-    float a0 = acc[0][d], a1 = acc[1][d];
-    PNTF_DBG(48 + d, (f32x4{a0, a1, 0.f, 0.f}));
-    a0 += __shfl_xor(a0, 16);
-    a1 += __shfl_xor(a1, 16);
-    a0 += __shfl_xor(a0, 32);
-    a1 += __shfl_xor(a1, 32);
-    PNTF_DBG(56 + d, (f32x4{a0, a1, 0.f, 0.f}));
-    ds[d] = a0;
-    dg[d] = a1;
+    float a0v = acc[0][d], a1v = acc[1][d];
+    a0v += __shfl_xor(a0v, 16);
+    a1v += __shfl_xor(a1v, 16);
+    a0v += __shfl_xor(a0v, 32);
+    a1v += __shfl_xor(a1v, 32);
+    ds[d] = a0v;
+    dg[d] = a1v;
   }
+  PNTF_STAMP(31);
 }
 
 // ---------------------------------------------------------------- epilogues (A9/A10)
@@ -628,14 +897,23 @@ __device__ __forceinline__ void field_body(const FieldArgs& a, int slot, int nsl
   const int lane = threadIdx.x & 63;
   const int64_t ntiles = (a.n + TILE - 1) / TILE;
   const Scratch sc = make_scratch(GRAD ? a.ws + (int64_t)slot * SCRATCH_FLOATS_PER_WAVE : nullptr);
+  const Rsrc W = make_rsrc(a.P, PACKED_FLOATS * 4);
   const float nan = __builtin_nanf("");
+  Ring ring;
+  ring_fill<2>(ring, W, lane * 16, E0Head{});
   for (int64_t tile = slot; tile < ntiles; tile += nslots) {
     f32x4 X[16], Y[16];
+    Carry cy;
     const int64_t pair = tile * TILE + (lane & 15);
     PairIO io;
     const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
-    float tau = forward_pass<DIM, GRAD>(a.P, io, X, Y, sc, a.compat, lane);
+    float tau;
+    if constexpr (GRAD)
+      tau = forward_pass<DIM, true, 4>(ring, a.P, io, X, Y, cy, sc, a.compat, lane, bwd_head());
+    else
+      tau = forward_pass<DIM, false, 2>(ring, a.P, io, X, Y, cy, sc, a.compat, lane, E0Head{});
     if (GRAD) drain_stores();
+    PNTF_STAMP(16);
     const bool store = (lane < 16) && pair < a.n;
     if (!ok) tau = nan;
     if (KIND == K_TAU) {
@@ -650,7 +928,7 @@ __device__ __forceinline__ void field_body(const FieldArgs& a, int slot, int nsl
       if (store) a.out0[pair] = sqrtf(T0sq) / tau;
     } else {
       float ds[DIM], dg[DIM];
-      backward_pass<DIM>(a.P, io, tau, X, Y, sc, lane, ds, dg);
+      backward_pass<DIM, 2>(ring, a.P, io, tau, X, Y, cy, sc, lane, ds, dg, E0Head{});
       if (KIND == K_TAU_GRAD) {
         if (store) {
           a.out0[pair] = tau;
@@ -702,10 +980,14 @@ __global__ __launch_bounds__(256, WAVES_PER_SIMD) void plan_kernel(PlanArgs a) {
   const int nslots = gridDim.x * WAVES;
   const int64_t ntiles = (a.q + TILE - 1) / TILE;
   const Scratch sc = make_scratch(a.ws + (int64_t)slot * SCRATCH_FLOATS_PER_WAVE);
+  const Rsrc W = make_rsrc(a.P, PACKED_FLOATS * 4);
   const int cap = a.max_iter + 1;
   const int64_t rows = (int64_t)cap + 1;
+  Ring ring;
+  ring_fill<2>(ring, W, lane * 16, E0Head{});
   for (int64_t tile = slot; tile < ntiles; tile += nslots) {
     f32x4 X[16], Y[16];
+    Carry cy;
     const int64_t qi = tile * TILE + (lane & 15);
     PairIO io;
     const bool ok = load_pair<DIM>(a.xp0, a.Btab, a.env, a.q, a.n_env, qi, io);
@@ -731,10 +1013,11 @@ __global__ __launch_bounds__(256, WAVES_PER_SIMD) void plan_kernel(PlanArgs a) {
     int it = 0;
     for (; it < cap; ++it) {
       if (!__any(active)) break;
-      float tau = forward_pass<DIM, true>(a.P, io, X, Y, sc, a.compat, lane);
+      float tau = forward_pass<DIM, true, 4>(ring, a.P, io, X, Y, cy, sc, a.compat, lane,
+                                             bwd_head());
       drain_stores();
       float ds[DIM], dg[DIM], vs[DIM], vg[DIM];
-      backward_pass<DIM>(a.P, io, tau, X, Y, sc, lane, ds, dg);
+      backward_pass<DIM, 2>(ring, a.P, io, tau, X, Y, cy, sc, lane, ds, dg, E0Head{});
       path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
       if (active) {
 #pragma unroll

@@ -20,30 +20,45 @@
 namespace pntf {
 
 // (J, L) <- [act](A·(J, L) (+ residual)) with σ tiles sig0 + ot of the value pass.
-// in: J tiles in[0..KT), L tiles in[KT..2KT); out likewise with OT.
+// in: J tiles in[0..KT), L tiles in[KT..2KT); out likewise with OT.  Epilogues are deferred
+// into the next group (layer()); the σ tile of a group is fetched when the group starts.
+template <int OT_, int KT_, bool RES, bool ACT, int NOUT>
+struct TaylorL {
+  static constexpr int OT = OT_, KT = KT_, NC = 2, NO = 1;
+  f32x4 (&out)[NOUT];
+  Scratch sc;
+  int sig0, lane;
+  f32x4 g[2];
+  f32x4 pend[1][2];
+  __device__ __forceinline__ void init(int ot, f32x4 (&acc)[1][2]) {
+    if (ACT) g[ot & 1] = load_tile(sc, sig0 + ot, lane);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[0][c] = RES ? out[c * OT + ot] : zero4();
+  }
+  __device__ __forceinline__ void epi(int t, int c, int h, const f32x4 (&v)[2]) {
+    const f32x4 gg = g[t & 1];
+#pragma unroll
+    for (int r = h * EP_ROWS; r < (h + 1) * EP_ROWS; ++r) {
+      const float J = v[0][r], L = v[1][r];
+      if (!ACT)
+        out[c * OT + t][r] = v[c][r];
+      else if (c == 0)
+        out[t][r] = gg[r] * J;                                                // :686
+      else
+        out[OT + t][r] = (10.f * gg[r] * (1.f - gg[r])) * J * J + gg[r] * L;  // :682-684
+    }
+  }
+};
+
 template <int OT, int KT, bool RES, bool ACT, int NIN, int NOUT>
 __device__ __forceinline__ void taylor_layer(Rsrc W, int wbase, const f32x4 (&in)[NIN],
                                              f32x4 (&out)[NOUT], Scratch sc, int sig0,
                                              int lane) {
-  f32x4 g;
-  layer<OT, KT, 2, SITE_TAYLOR>(
-      W, wbase, in, lane,
-      [&](int ot, f32x4 (&acc)[1][2]) {
-        if (ACT) g = load_tile(sc, sig0 + ot, lane);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) acc[0][c] = RES ? out[c * OT + ot] : f32x4{0.f, 0.f, 0.f, 0.f};
-      },
-      [&](int ot, f32x4 (&acc)[1][2]) {
-        const f32x4 J = acc[0][0], L = acc[0][1];
-        if (ACT) {
-          const f32x4 gp = 10.f * g * (1.f - g);                     // DSigmoid (:89-96)
-          out[ot] = g * J;                                           // act_laplace :686
-          out[OT + ot] = gp * J * J + g * L;                         // :682-684
-        } else {
-          out[ot] = J;
-          out[OT + ot] = L;
-        }
-      });
+  TaylorL<OT, KT, RES, ACT, NOUT> ly{out, sc, sig0, lane};
+  Ring ring;
+  ring_fill<2>(ring, W, lane * 16, Head<KT, 2>{wbase});
+  layer<OT, KT, 2, 2, SITE_TAYLOR, 0>(ring, W, wbase, in, lane, ly, NoPre{}, NoNext{});
+  flush(ly);
 }
 
 // One direction k = p*DIM + d (p = 0 start, 1 goal point).  Returns (∂τ/∂x_k, ∂²τ/∂x_k²),
@@ -65,13 +80,13 @@ __device__ __forceinline__ void taylor_direction(Rsrc W, const PairIO& io, int p
   for (int i = 0; i < 16; ++i) TX[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     f32x4 js, jc, ls, lc;   // J/L rows of the sin part and the cos part of feature tile kt
-    pipelined<64, 2, PF_STEPS, SITE_TAYLOR>(
+    pipelined<64, 2, SITE_TAYLOR>(
         W, lane * 16,
         [&](int st, int l) { return frag<16>(F + OFF_E0 * 4, st % 8, st / 8 + 8 * l); },
         [&](auto st, const f32x4 (&a)[2]) {
           constexpr int kt = decltype(st)::value / 8, ot = decltype(st)::value % 8;
           if constexpr (ot == 0) {
-            f32x4 q = f32x4{0.f, 0.f, 0.f, 0.f}, wd = f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 q = zero4(), wd = zero4();
 #pragma unroll
             for (int j = 0; j < DIM; ++j) {
               f32x4 wj = TWO_PI * ld4(io.Bw + j * H + 16 * kt + 4 * g);
@@ -180,7 +195,10 @@ __device__ __forceinline__ void residual_body(const ResidualArgs& a, int slot, i
     float tau;
     {
       f32x4 X[16], Y[16];
-      tau = forward_pass<DIM, true>(a.P, io, X, Y, sc, 0, lane);
+      Carry cy;
+      Ring ring;
+      ring_fill<2>(ring, W, lane * 16, E0Head{});
+      tau = forward_pass<DIM, true, 0>(ring, a.P, io, X, Y, cy, sc, 0, lane, NoNext{});
     }
     drain_stores();
     float D[DIM];

@@ -44,7 +44,10 @@ PACKED_FP32 = re.compile(r"\bv_pk_(mul|add|fma)_f32\b")
 UNITS = (
     [("field_d%d_k%d" % (d, k), "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k])
      for d in (3, 6) for k in range(5)]
-    + [("plan_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN"]) for d in (3, 6)]
+    # plan_kernel<6> holds the 6-dof path state beside the ring: a 2-step ring keeps it
+    # spill-free (the 4-step ring spills 2 VGPRs there).
+    + [("plan_d3", "pntf_kernels.hip", ["-DPNTF_DIM=3", "-DPNTF_PLAN"]),
+       ("plan_d6", "pntf_kernels.hip", ["-DPNTF_DIM=6", "-DPNTF_PLAN", "-DPNTF_PF_STEPS=2"])]
     + [("residual_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_RESIDUAL"])
        for d in (3, 6)]
     + [("util", "pntf_kernels.hip", ["-DPNTF_UTIL"]), ("capi", "pntf_capi.hip", [])]

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/../.."
 build() {
   local name=$1; shift
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -Iinclude \
-    -Ip-ntfields_amd/csrc "$@" tests/diag/perf_variant.hip -o tests/diag/libperf_$name.so \
+    -Ip-ntfields_amd/csrc -Xclang -target-feature -Xclang -packed-fp32-ops "$@" tests/diag/perf_variant.hip -o tests/diag/libperf_$name.so \
     -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "VGPRs:|AGPRs|Spill" | tr '\n' ' ' \
     | sed "s/^/$name: /"; echo
 }

@@ -17,3 +17,9 @@ extern "C" int perf_set_dbg(float* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(pntf::pntf_dbg), &p, sizeof(p)) == hipSuccess ? 0 : 1;
 }
 #endif
+
+#ifdef PNTF_DEBUG_STAMPS
+extern "C" int perf_set_stamps(unsigned long long* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(pntf::pntf_stamps), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+}
+#endif

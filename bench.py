@@ -209,14 +209,25 @@ def extras(packed, dev):
     xq = torch.from_numpy(synth.make_box_pairs(q, 6, seed=3)).to(dev)
     res = {}
 
-    def run_plan():
+    def run_plan(schedule):
         res["p"] = ops.plan(packed, xq, Ba, dim=6, step=0.015, tol=0.03, max_iter=199,
-                            mode=ops.GRAD_EXACT)
-    ms = timeit(run_plan, reps=2)
+                            mode=ops.GRAD_EXACT, schedule=schedule)
+    ms = timeit(lambda: run_plan("auto"), reps=2)
     steps = res["p"][1].cpu().numpy()
     out["c5_arm_plan_1024q_ms"] = ms
     out["c5_arm_plan_query_steps_per_s"] = float(steps.sum()) / (ms * 1e-3)
     out["c5_arm_plan_mean_steps"] = float(steps.mean())
+    out["c5_arm_plan_max_steps"] = int(steps.max())
+    out["c5_arm_plan_1024q_wave_tile_ms"] = timeit(lambda: run_plan("wave_tile"), reps=2)
+    # batch-1 Gibson planner (test/gib_plan.py runs Q = 1): device time per loop step
+    x1 = torch.from_numpy(synth.make_pairs(1, 3, seed=21)).to(dev)
+    B1 = torch.from_numpy(synth.make_B(3, seed=1)).to(dev)
+    for sched in ("auto", "wave_tile"):
+        def run1():
+            res["p1"] = ops.plan(packed, x1, B1, dim=3, step=0.03, tol=1e-9, max_iter=99,
+                                 mode=ops.GRAD_BACKGRAD_COMPAT, schedule=sched)
+        ms = timeit(run1, reps=2)
+        out["gib_plan_q1_ms_per_step_" + sched] = ms / 100.0
     return out
 
 

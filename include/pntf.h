@@ -42,6 +42,11 @@ typedef enum {
 /* Gradient flavours for the reverse sweep. */
 #define PNTF_GRAD_EXACT 0            /* == Model.gradient(NN.out) autograd (:890-896)     */
 #define PNTF_GRAD_BACKGRAD_COMPAT 1  /* == NN.out_backgrad incl. its encoder[0] quirk     */
+
+/* Planner schedules (pntf_plan_ex). */
+#define PNTF_SCHED_AUTO 0
+#define PNTF_SCHED_WAVE_TILE 1
+#define PNTF_SCHED_SPLIT_TILE 2
                                      /*    (model_res_sigmoid_multi.py:402-647, :435-438) */
 
 int pntf_abi_version(void);
@@ -98,6 +103,17 @@ int pntf_plan(const float* packed, int dim, const float* xp0, int64_t q, const f
               const int32_t* env, int32_t n_env, int mode, float step, float tol,
               int32_t max_iter, float* path, int32_t* steps, void* ws, size_t ws_bytes,
               hipStream_t stream);
+
+/* pntf_plan with an explicit schedule (pntf_plan uses PNTF_SCHED_AUTO):
+ *   PNTF_SCHED_WAVE_TILE   one wave per 16-query tile (throughput: many queries);
+ *   PNTF_SCHED_SPLIT_TILE  the 4 waves of a workgroup share a tile, each computing a quarter
+ *                          of every layer's outputs (latency: few queries, down to q = 1);
+ *   PNTF_SCHED_AUTO        split while ceil(q/16) <= 2 x the device's CU count.
+ * Results agree between schedules to fp32 rounding (the cross-wave sums are reordered). */
+int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, const float* Btab,
+                 const int32_t* env, int32_t n_env, int mode, float step, float tol,
+                 int32_t max_iter, float* path, int32_t* steps, void* ws, size_t ws_bytes,
+                 int schedule, hipStream_t stream);
 
 /* Eikonal residual: NN.out_laplace + the per-pair residual of Model.Loss
  * (model_res_sigmoid_multi.py:710-848, :897-946), Taylor mode.  Each output may be NULL:

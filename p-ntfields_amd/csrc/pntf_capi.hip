@@ -15,6 +15,8 @@ __global__ void field_kernel(FieldArgs a);
 template <int DIM>
 __global__ void plan_kernel(PlanArgs a);
 template <int DIM>
+__global__ void plan_split_kernel(PlanArgs a);
+template <int DIM>
 __global__ void residual_kernel(ResidualArgs a);
 __global__ void sum_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ out);
 __global__ void pack_kernel(const float* __restrict__ src, int rows, int cols, int ld,
@@ -59,8 +61,15 @@ static int64_t grid_for(int64_t n) {
   return wgs < cap ? (wgs < 1 ? 1 : wgs) : cap;
 }
 
-static int grid_with_ws(int64_t n, size_t ws_bytes, int64_t* grid) {
-  int64_t g = grid_for(n);
+// split-tile grid (pntf_split.h): one 4-wave workgroup per pair tile, at most one per CU
+static int64_t split_grid_for(int64_t n) {
+  int64_t ntiles = (n + TILE - 1) / TILE;
+  int64_t cap = (int64_t)num_cus() * WG_PER_CU;
+  return ntiles < cap ? (ntiles < 1 ? 1 : ntiles) : cap;
+}
+
+static int grid_with_ws(int64_t n, size_t ws_bytes, int64_t* grid, bool split = false) {
+  int64_t g = split ? split_grid_for(n) : grid_for(n);
   int64_t fit = (int64_t)(ws_bytes / (SLOT_BYTES * WAVES));
   if (fit < 1) return fail(PNTF_ERR_WORKSPACE, "workspace too small (%s)", "need >= 4 slots");
   *grid = g < fit ? g : fit;
@@ -133,7 +142,8 @@ size_t pntf_packed_floats(void) { return (size_t)PACKED_FLOATS; }
 
 size_t pntf_workspace_bytes(int64_t n) {
   if (n <= 0) n = 1;
-  return (size_t)grid_for(n) * WAVES * SLOT_BYTES;
+  int64_t g = grid_for(n), gs = split_grid_for(n);
+  return (size_t)(g > gs ? g : gs) * WAVES * SLOT_BYTES;
 }
 
 int pntf_pack_weights(const float* const* params, int n_params, float* packed,
@@ -222,23 +232,44 @@ int pntf_plan(const float* packed, int dim, const float* xp0, int64_t q, const f
               const int32_t* env, int32_t n_env, int mode, float step, float tol,
               int32_t max_iter, float* path, int32_t* steps, void* ws, size_t ws_bytes,
               hipStream_t stream) {
+  return pntf_plan_ex(packed, dim, xp0, q, Btab, env, n_env, mode, step, tol, max_iter, path,
+                      steps, ws, ws_bytes, PNTF_SCHED_AUTO, stream);
+}
+
+int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, const float* Btab,
+                 const int32_t* env, int32_t n_env, int mode, float step, float tol,
+                 int32_t max_iter, float* path, int32_t* steps, void* ws, size_t ws_bytes,
+                 int schedule, hipStream_t stream) {
   int st = check_common(packed, dim, xp0, q, Btab, n_env);
   if (st) return st;
   if (max_iter < 0) return fail(PNTF_ERR_ARG, "max_iter must be >= 0%s");
   if (mode != PNTF_GRAD_EXACT && mode != PNTF_GRAD_BACKGRAD_COMPAT)
     return fail(PNTF_ERR_ARG, "unknown gradient mode%s");
+  if (schedule != PNTF_SCHED_AUTO && schedule != PNTF_SCHED_WAVE_TILE &&
+      schedule != PNTF_SCHED_SPLIT_TILE)
+    return fail(PNTF_ERR_ARG, "unknown schedule%s");
   if (q == 0) return PNTF_OK;
   if (!path || !steps) return fail(PNTF_ERR_ARG, "null output%s");
   if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
+  // Split tiles while every tile still gets a CU of its own or shares one with at most one
+  // other (a split step is ~3x faster than a one-wave step; the one-wave kernel wins once
+  // the tiles fill every SIMD).
+  const int64_t ntiles = (q + TILE - 1) / TILE;
+  const bool split = schedule == PNTF_SCHED_SPLIT_TILE ||
+                     (schedule == PNTF_SCHED_AUTO && ntiles <= 2 * (int64_t)num_cus());
   int64_t grid;
-  st = grid_with_ws(q, ws_bytes, &grid);
+  st = grid_with_ws(q, ws_bytes, &grid, split);
   if (st) return st;
   PlanArgs a{packed, xp0, Btab, env, q, n_env, mode, step, tol, max_iter, path, steps,
              (float*)ws};
-  if (dim == 3)
-    hipLaunchKernelGGL((plan_kernel<3>), dim3((unsigned)grid), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL((plan_kernel<6>), dim3((unsigned)grid), dim3(256), 0, stream, a);
+  dim3 g((unsigned)grid), b(256);
+  if (split) {
+    if (dim == 3) hipLaunchKernelGGL((plan_split_kernel<3>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((plan_split_kernel<6>), g, b, 0, stream, a);
+    return check_launch("plan_split_kernel");
+  }
+  if (dim == 3) hipLaunchKernelGGL((plan_kernel<3>), g, b, 0, stream, a);
+  else hipLaunchKernelGGL((plan_kernel<6>), g, b, 0, stream, a);
   return check_launch("plan_kernel");
 }
 

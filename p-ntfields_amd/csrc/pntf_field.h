@@ -273,8 +273,10 @@ __device__ unsigned long long* pntf_stamps;
 #define PNTF_STAMP(idx)
 #endif
 
-template <int NC>
-constexpr int out_group() { return NC == 1 ? PNTF_NO1 : 1; }
+// Out tiles per MFMA group: PNTF_NO1 for single-column layers, capped at the layer's out
+// tiles (the out-tile-split kernels of pntf_split.h run layers of 2 local out tiles).
+template <int NC, int OT = 16>
+constexpr int out_group() { return NC == 1 ? (OT < PNTF_NO1 ? OT : PNTF_NO1) : 1; }
 
 // "No previous layer tail" hook.
 struct NoPre {
@@ -305,7 +307,8 @@ template <int OT, int KT, int NC, int KS, int SITE, int NLN, int NIN, class L, c
           class NextF>
 __device__ __forceinline__ void layer(Ring& ring, Rsrc W, int wbase, const f32x4 (&in)[NIN],
                                       int lane, L& ly, PreF pre, NextF naddr) {
-  constexpr int NO = out_group<NC>();
+  constexpr int NO = L::NO;
+  static_assert(L::OT == OT && L::NC == NC, "layer object shape");
   constexpr int GS = KT / KS;                 // steps per group
   constexpr int STEPS = (OT / NO) * GS;
   constexpr int UNITS = NO * NC * EP_SPLIT;   // deferred epilogue units per group
@@ -370,7 +373,7 @@ __device__ __forceinline__ void flush(L& ly) {
 // scratch tile sc0 + c*OT + t when SAVE, and kept in keep[t] when KEEP (single column).
 template <int OT_, int KT_, int NC_, bool RES, bool SAVE, bool KEEP = false>
 struct FwdAct {
-  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_>();
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_, OT_>();
   Rsrc W;
   int bias;
   f32x4 (&out)[16];
@@ -407,7 +410,7 @@ struct FwdAct {
 // out[c*OT+t] = A·in + bias, no activation (encoder[-1], :234).
 template <int OT_, int KT_, int NC_>
 struct FwdLin {
-  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_>();
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_, OT_>();
   Rsrc W;
   int bias;
   f32x4 (&out)[16];
@@ -433,7 +436,7 @@ struct FwdLin {
 // Reverse: out[c*OT+t] = (A^T·in (+ out[c*OT+t] if RES)) ⊙ scratch[mul0 + c*OT + t] (if MUL)
 template <int OT_, int KT_, int NC_, bool RES, bool MUL>
 struct Bwd {
-  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_>();
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_, OT_>();
   f32x4 (&out)[16];
   Scratch sc;
   int mul0, lane;

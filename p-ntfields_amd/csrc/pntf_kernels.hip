@@ -1,8 +1,10 @@
 // One kernel per translation unit, selected at build time (pntf/build.py):
 //   -DPNTF_KIND=0..4 -DPNTF_DIM=3|6   field_kernel<DIM, KIND>
 //   -DPNTF_PLAN -DPNTF_DIM=3|6         plan_kernel<DIM>
+//   -DPNTF_PLAN_SPLIT -DPNTF_DIM=3|6   plan_split_kernel<DIM> (pntf_split.h)
 //   -DPNTF_RESIDUAL -DPNTF_DIM=3|6     residual_kernel<DIM> (Taylor mode, pntf_taylor.h)
 //   -DPNTF_UTIL                        pack_kernel, copy_kernel, sum_kernel
+#include "pntf_split.h"
 #include "pntf_taylor.h"
 
 namespace pntf {
@@ -10,6 +12,8 @@ namespace pntf {
 template __global__ void field_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
 #elif defined(PNTF_PLAN)
 template __global__ void plan_kernel<PNTF_DIM>(PlanArgs);
+#elif defined(PNTF_PLAN_SPLIT)
+template __global__ void plan_split_kernel<PNTF_DIM>(PlanArgs);
 #elif defined(PNTF_RESIDUAL)
 template __global__ void residual_kernel<PNTF_DIM>(ResidualArgs);
 #endif

@@ -1,0 +1,561 @@
+#pragma once
+// Out-tile-split τ / ∇τ passes for latency-bound batches ("split kernels").
+//
+// The throughput kernels of pntf_field.h give one wave a whole 16-pair tile, so a batch of q
+// pairs keeps only ceil(q/16) SIMDs busy: the 1024-query arm planner (BASELINE config C5)
+// ran on 64 of the chip's 1024 SIMDs, and a batch-1 planner step (test/gib_plan.py, Q = 1)
+// on one.  Here the four waves of a workgroup (one per SIMD) share one pair tile instead:
+//   * wave w computes out tiles [w·OT/4, (w+1)·OT/4) of every layer (the packed fragments
+//     of those tiles are contiguous, so the weight stream is the same ring as before with a
+//     per-wave scalar base offset);
+//   * its output tiles go to LDS, one s_barrier, and every wave reads the whole activation
+//     back as the next layer's B operand (the register tile layout is the LDS layout:
+//     1 KiB per tile, 16 B per lane, conflict-free ds_read_b128 / ds_write_b128);
+//   * residual inputs are the wave's own slice of the block input, picked from the full
+//     register bank before it is overwritten (uniform selects, no LDS);
+//   * saved σ10 tiles stay per wave in its scratch slot: a feature tile is owned by the same
+//     wave in the forward and the reverse sweep, so each wave reads back only what it wrote;
+//   * the head dot product and the Fourier fold are reduced across the 4 waves through LDS
+//     in a fixed order, so every wave holds the same τ and ∇τ (the planner's freeze test and
+//     loop exit are wave-uniform and identical in all four waves).
+// Per layer each wave does a quarter of the MFMAs plus one 16 KiB LDS read, so a planner
+// step takes about a third of the one-wave time.
+#include "pntf_field.h"
+
+namespace pntf {
+
+constexpr int SPLIT = WAVES;                  // waves sharing a pair tile
+constexpr int XBUF_FLOATS = 16 * 256;         // one activation: 16 tiles x 64 lanes x 4
+constexpr int RED_FLOATS = SPLIT * 12 * 64;   // cross-wave partial sums (≤ 2·DIM per lane)
+constexpr int SPLIT_LDS_FLOATS = 2 * XBUF_FLOATS + RED_FLOATS;
+
+typedef __attribute__((address_space(3))) float lds_f;
+typedef __attribute__((address_space(3))) f32x4 lds_f4;
+
+// Every wave's LDS writes done, then the workgroup barrier.  Written as one asm block with
+// a memory clobber: the s_barrier builtin alone is not a compiler barrier for LDS accesses.
+__device__ __forceinline__ void wg_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+struct Split {
+  lds_f* lds;
+  int w, lane;
+  __device__ lds_f4* tile(int buf, int t) const {
+    return reinterpret_cast<lds_f4*>(lds + buf * XBUF_FLOATS + t * 256 + lane * 4);
+  }
+  __device__ lds_f* red(int wave, int j) const {
+    return lds + 2 * XBUF_FLOATS + (wave * 12 + j) * 64 + lane;
+  }
+};
+
+// Local out tiles L[c·OTL + t] (global tile c·OTG + w·OTL + t) -> LDS buffer -> every
+// wave's full bank X[0 .. NC·OTG).
+template <int OTL, int NC>
+__device__ __forceinline__ void exchange(const Split& sp, int buf, const f32x4 (&L)[16],
+                                         f32x4 (&X)[16]) {
+  constexpr int OTG = OTL * SPLIT;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int t = 0; t < OTL; ++t) *sp.tile(buf, c * OTG + sp.w * OTL + t) = L[c * OTL + t];
+  wg_sync();
+#pragma unroll
+  for (int i = 0; i < NC * OTG; ++i) X[i] = *sp.tile(buf, i);
+}
+
+// The wave's slice of a full bank: R[c·OTL + t] = X[c·OTG + w·OTL + t] (w is uniform).
+template <int OTL, int NC>
+__device__ __forceinline__ void slice(const f32x4 (&X)[16], int w, f32x4 (&R)[16]) {
+  constexpr int OTG = OTL * SPLIT;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int t = 0; t < OTL; ++t) {
+      f32x4 v = X[c * OTG + t];
+#pragma unroll
+      for (int q = 1; q < SPLIT; ++q) {
+        // opaque condition: a select chain on w == q would otherwise be folded into a
+        // runtime-indexed X[.], which sends the whole bank to scratch
+        int m = w == q;
+        asm volatile("" : "+v"(m));
+        v = m ? X[c * OTG + q * OTL + t] : v;
+      }
+      R[c * OTL + t] = v;
+    }
+}
+
+// Sum of one value per lane over the 4 waves, in wave order (identical in every wave).
+template <int NV>
+__device__ __forceinline__ void reduce_waves(const Split& sp, float (&v)[NV]) {
+#pragma unroll
+  for (int j = 0; j < NV; ++j) *sp.red(sp.w, j) = v[j];
+  wg_sync();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    float s = *sp.red(0, j);
+#pragma unroll
+    for (int q = 1; q < SPLIT; ++q) s += *sp.red(q, j);
+    v[j] = s;
+  }
+}
+
+// Byte offset of wave w's first fragment in a packed (OTG x KT) layer.
+template <int OTG, int KT>
+__device__ __forceinline__ int wofs(int w) {
+  return w * (OTG / SPLIT) * KT * 1024;
+}
+
+// Ring head of the split forward pass: encoder[0], local out tiles 2w, 2w + 1; step j reads
+// fragments (local out tile j % 2, k tile j / 2 + 8 l).
+struct SE0Head {
+  int base;
+  __device__ int operator()(int j, int l) const {
+    return base + (((j % 2) * 16 + j / 2 + 8 * l) * 64) * 16;
+  }
+};
+__device__ __forceinline__ SE0Head se0_head(int w) {
+  return SE0Head{(OFF_FWD + OFF_E0) * 4 + wofs<8, 16>(w)};
+}
+
+struct SplitCarry {
+  f32x4 sg3[8];   // σ10 of generator[-2], local tiles 0, 1
+  f32x4 g4w[2];   // generator[-1].weight rows of local tiles 0, 1
+};
+
+// Split forward pass (NN.out, :215-259).  X is the full bank; returns τ (same in all waves).
+template <int DIM, bool GRAD, int NLA, class AfterF>
+__device__ __forceinline__ float split_forward(Ring& ring, const float* __restrict__ P,
+                                               const PairIO& io, f32x4 (&X)[16], SplitCarry& cy,
+                                               Scratch sc, int compat, const Split& sp,
+                                               AfterF after) {
+  const int lane = sp.lane, g = lane >> 4, w = sp.w;
+  const Rsrc W = make_rsrc(P, PACKED_FLOATS * 4);
+  constexpr int BB = OFF_BIAS * 4;
+  constexpr int F = OFF_FWD * 4;
+  const float cm = compat ? 1.f : 0.f;
+  f32x4 L[16], R[16];
+
+  // ---- encoder[0] on Fourier features (:186-190, :227): local out tiles ol = 0, 1 of both
+  // columns; every wave computes all 256 features (they are its B operand).
+  f32x4 eb[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) L[i] = zero4();
+  {
+    f32x4 sn[2], cs[2];
+    f32x4 bw[2][DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) bw[0][d] = ld4(io.Bw + d * H + 4 * g);
+    const int e0 = F + OFF_E0 * 4 + wofs<8, 16>(w);
+    const int we = F + OFF_EBLK * 4 + wofs<8, 8>(w);
+    run_steps<16, 2, 2, SITE_FWD_E0>(
+        ring, W, lane * 16, SE0Head{e0}, Head<8, 2>{we},
+        [&](auto st, const f32x4 (&a)[2]) {
+          constexpr int S = decltype(st)::value;
+          constexpr int kt = S / 2, ol = S % 2;
+          if constexpr (S == 1) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+              eb[t] = bload(W, g * 16, BB + (B_E0 + 16 * (2 * w + t)) * 4);
+          }
+          if constexpr (ol == 1 && kt < 7) {
+#pragma unroll
+            for (int d = 0; d < DIM; ++d)
+              bw[(kt + 1) & 1][d] = ld4(io.Bw + d * H + 16 * (kt + 1) + 4 * g);
+          }
+          if constexpr (ol == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int s = 0; s < 4; ++s) {
+                float q = 0.f;
+#pragma unroll
+                for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], TWO_PI * bw[kt & 1][d][s], q);
+                float x0, x1;
+                sincos_fast(q, x0, x1);
+                sn[c][s] = x0;
+                cs[c][s] = x1;
+              }
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) L[c * 2 + ol] = mfma(a[0][s], sn[c][s], L[c * 2 + ol]);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) L[c * 2 + ol] = mfma(a[1][s], cs[c][s], L[c * 2 + ol]);
+          }
+        });
+  }
+  // bias, softplus, σ (compat: the out_backgrad quirk :435-438 stores σ10(softplus(y)))
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int t = c * 2 + i;
+      f32x4 s, sg;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        SpSig v = sp_sig(L[t][r] + eb[i][r]);
+        s[r] = v.sp;
+        sg[r] = fmaf(cm, __builtin_amdgcn_rcpf(2.f - v.sg) - v.sg, v.sg);
+      }
+      L[t] = s;
+      if (GRAD) store_tile(sc, T_E0 + t, lane, sg);
+    }
+  exchange<2, 2>(sp, 0, L, X);
+
+  // ---- encoder residual blocks (:228-232)
+  const int BE = BB + B_EBLK * 4 + w * 2 * 16 * 4;
+  const int WE = F + OFF_EBLK * 4 + wofs<8, 8>(w);
+  {
+    slice<2, 2>(X, w, R);
+    FwdAct<2, 8, 2, false, GRAD> a0{W, BE, L, sc, T_EBLK, lane, cy.sg3};
+    layer<2, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE, X, lane, a0, NoPre{},
+                                        Head<8, 2>{WE + SZ_E * 4});
+    flush(a0);
+    exchange<2, 2>(sp, 1, L, X);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L[i] = R[i];
+    FwdAct<2, 8, 2, true, GRAD> b0{W, BE + 128 * 4, L, sc, T_EBLK + 16, lane, cy.sg3};
+    layer<2, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + SZ_E * 4, X, lane, b0, NoPre{},
+                                        Head<8, 2>{WE + 2 * SZ_E * 4});
+    flush(b0);
+    exchange<2, 2>(sp, 0, L, X);
+  }
+  {
+    slice<2, 2>(X, w, R);
+    FwdAct<2, 8, 2, false, GRAD> a1{W, BE + 256 * 4, L, sc, T_EBLK + 32, lane, cy.sg3};
+    layer<2, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
+                                        Head<8, 2>{WE + 3 * SZ_E * 4});
+    flush(a1);
+    exchange<2, 2>(sp, 1, L, X);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L[i] = R[i];
+    FwdAct<2, 8, 2, true, GRAD> b1{W, BE + 384 * 4, L, sc, T_EBLK + 48, lane, cy.sg3};
+    layer<2, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, X, lane, b1, NoPre{},
+                                        Head<8, 2>{F + OFF_E3 * 4 + wofs<8, 8>(w)});
+    flush(b1);
+    exchange<2, 2>(sp, 0, L, X);
+  }
+  // ---- encoder[-1] (:234) -> X = [zs | zg]
+  {
+    FwdLin<2, 8, 2> e3{W, BB + (B_E3 + 2 * 16 * w) * 4, L, lane};
+    layer<2, 8, 2, 2, SITE_FWD_ENC, 4>(ring, W, F + OFF_E3 * 4 + wofs<8, 8>(w), X, lane, e3,
+                                        NoPre{}, Head<16>{F + OFF_GBLK * 4 + wofs<16, 16>(w)});
+    flush(e3);
+    exchange<2, 2>(sp, 1, L, X);
+  }
+
+  // ---- merge (:236-244), in place and redundantly in every wave: X = u = [M | m]
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    f32x4 s0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float zs = X[t][r], zg = X[8 + t][r];
+      float d = zs - zg;
+      float e = exp_neg10abs(d);
+      float cc = 0.1f * log1p_small(e);
+      X[t][r] = fmaxf(zs, zg) + cc;
+      X[8 + t][r] = fminf(zs, zg) - cc;
+      float rr = __builtin_amdgcn_rcpf(1.f + e);
+      s0[r] = (d >= 0.f) ? rr : e * rr;
+    }
+    if (GRAD) store_tile(sc, T_S0 + t, lane, s0);
+  }
+
+  // ---- generator residual blocks (:246-249)
+#pragma unroll 1
+  for (int i = 0; i < 3; ++i) {
+    const int wa = opaque(F + (OFF_GBLK + (2 * i) * SZ_G) * 4 + wofs<16, 16>(w));
+    const int wb = opaque(F + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4 + wofs<16, 16>(w));
+    const int wn = opaque(i < 2 ? F + (OFF_GBLK + (2 * i + 2) * SZ_G) * 4 + wofs<16, 16>(w)
+                                : F + OFF_G3 * 4 + wofs<8, 16>(w));
+    const int bg = BB + (B_GBLK + (2 * i) * 256 + 4 * 16 * w) * 4;
+    slice<4, 1>(X, w, R);
+    FwdAct<4, 16, 1, false, GRAD> ga{W, bg, L, sc, T_GBLK + 32 * i, lane, cy.sg3};
+    layer<4, 16, 1, 1, SITE_FWD_GEN, 4>(ring, W, wa, X, lane, ga, NoPre{}, Head<16>{wb});
+    flush(ga);
+    exchange<4, 1>(sp, 0, L, X);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) L[t] = R[t];
+    FwdAct<4, 16, 1, true, GRAD> gb{W, bg + 256 * 4, L, sc, T_GBLK + 32 * i + 16, lane, cy.sg3};
+    // the last block hands over to generator[-2], 2 local out tiles per step
+    if (i < 2)
+      layer<4, 16, 1, 1, SITE_FWD_GEN, 4>(ring, W, wb, X, lane, gb, NoPre{}, Head<16>{wn});
+    else
+      layer<4, 16, 1, 1, SITE_FWD_GEN, 2>(ring, W, wb, X, lane, gb, NoPre{}, Head<16>{wn});
+    flush(gb);
+    exchange<4, 1>(sp, 1, L, X);
+  }
+
+  // ---- generator[-2] + act (:251-252): local tiles L[0..1], σ kept for the reverse sweep
+#pragma unroll
+  for (int t = 0; t < 2; ++t) cy.g4w[t] = bload(W, g * 16, BB + (B_G4W + 16 * (2 * w + t)) * 4);
+  const float g4b = bload(W, 0, BB + B_G4B * 4)[0];
+  {
+    FwdAct<2, 16, 1, false, GRAD, GRAD> g3{W, BB + (B_G3 + 2 * 16 * w) * 4, L, sc, T_G3, lane,
+                                           cy.sg3};
+    layer<2, 16, 1, 1, SITE_FWD_GEN, NLA>(ring, W, F + OFF_G3 * 4 + wofs<8, 16>(w), X, lane, g3,
+                                          NoPre{}, after);
+    flush(g3);
+  }
+  // ---- head (:254-255): partial dot of the local tiles, summed over the waves
+  float part[1] = {0.f};
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) part[0] = fmaf(cy.g4w[t][s], L[t][s], part[0]);
+  part[0] += __shfl_xor(part[0], 16);
+  part[0] += __shfl_xor(part[0], 32);
+  reduce_waves<1>(sp, part);
+  const float y4 = part[0] + g4b;
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-0.144269504088896341f * y4));
+}
+
+// Split reverse sweep (exact, or out_backgrad when the forward stored the quirk).  On entry
+// the ring holds the G3^T head of this wave; on return the first PF steps of `after`.
+template <int DIM, int NLA, class AfterF>
+__device__ __forceinline__ void split_backward(Ring& ring, const float* __restrict__ P,
+                                               const PairIO& io, float tau, f32x4 (&X)[16],
+                                               const SplitCarry& cy, Scratch sc, const Split& sp,
+                                               float (&ds)[DIM], float (&dg)[DIM],
+                                               AfterF after) {
+  const int lane = sp.lane, g = lane >> 4, w = sp.w;
+  const Rsrc W = make_rsrc(P, PACKED_FLOATS * 4);
+  constexpr int Bk = OFF_BWD * 4;
+  f32x4 L[16], R[16];
+
+  // ---- head and generator[-2] (:592-613): dv = d · G4 ⊙ σ10(y3), local tiles -> X[0..7]
+  const float dd = 0.1f * tau * (1.f - tau);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) L[t] = (dd * cy.g4w[t]) * cy.sg3[t];
+  exchange<2, 1>(sp, 0, L, X);
+  // du = G3^T dv ⊙ σ10(y2 of generator block 2)   (G3^T: 256 x 128, OT 16, KT 8)
+  {
+    Bwd<4, 8, 1, false, true> l{L, sc, T_GBLK + 32 * 2 + 16, lane};
+    layer<4, 8, 1, 1, SITE_BWD_GEN, 4>(ring, W, Bk + OFF_G3 * 4 + wofs<16, 8>(w), X, lane, l,
+                                       NoPre{},
+                                       Head<16>{Bk + (OFF_GBLK + 5 * SZ_G) * 4 + wofs<16, 16>(w)});
+    flush(l);
+    exchange<4, 1>(sp, 1, L, X);
+  }
+  // ---- generator blocks, reverse (:615-618)
+#pragma unroll 1
+  for (int i = 2; i >= 0; --i) {
+    const int wa = opaque(Bk + (OFF_GBLK + (2 * i) * SZ_G) * 4 + wofs<16, 16>(w));
+    const int wb = opaque(Bk + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4 + wofs<16, 16>(w));
+    slice<4, 1>(X, w, R);   // dr
+    Bwd<4, 16, 1, false, true> lb{L, sc, T_GBLK + 32 * i, lane};
+    layer<4, 16, 1, 1, SITE_BWD_GEN, 4>(ring, W, wb, X, lane, lb, NoPre{}, Head<16>{wa});
+    flush(lb);
+    exchange<4, 1>(sp, 0, L, X);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) L[t] = R[t];
+    if (i > 0) {
+      const int wn = opaque(Bk + (OFF_GBLK + (2 * i - 1) * SZ_G) * 4 + wofs<16, 16>(w));
+      Bwd<4, 16, 1, true, true> la{L, sc, T_GBLK + 32 * (i - 1) + 16, lane};
+      layer<4, 16, 1, 1, SITE_BWD_GEN, 4>(ring, W, wa, X, lane, la, NoPre{}, Head<16>{wn});
+      flush(la);
+    } else {
+      Bwd<4, 16, 1, true, false> la{L, sc, 0, lane};
+      layer<4, 16, 1, 1, SITE_BWD_GEN, 2>(ring, W, wa, X, lane, la, NoPre{},
+                                          Head<8, 2>{Bk + OFF_E3 * 4 + wofs<8, 8>(w)});
+      flush(la);
+    }
+    exchange<4, 1>(sp, 1, L, X);
+  }
+  // ---- merge Jacobian (:620-627), redundantly in every wave: X = [dzs | dzg]
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    f32x4 s0 = load_tile(sc, T_S0 + t, lane);
+    f32x4 s1 = 1.f - s0;
+    f32x4 dM = X[t], dm = X[8 + t];
+    X[t] = s0 * dM + s1 * dm;
+    X[8 + t] = s1 * dM + s0 * dm;
+  }
+  // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1)
+  const int WE = Bk + OFF_EBLK * 4 + wofs<8, 8>(w);
+  {
+    Bwd<2, 8, 2, false, true> e3{L, sc, T_EBLK + 32 * 1 + 16, lane};
+    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, Bk + OFF_E3 * 4 + wofs<8, 8>(w), X, lane, e3,
+                                       NoPre{}, Head<8, 2>{WE + 3 * SZ_E * 4});
+    flush(e3);
+    exchange<2, 2>(sp, 0, L, X);
+  }
+  // ---- encoder blocks, reverse (:633-636)
+  {
+    slice<2, 2>(X, w, R);
+    Bwd<2, 8, 2, false, true> b1{L, sc, T_EBLK + 32, lane};
+    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, X, lane, b1, NoPre{},
+                                       Head<8, 2>{WE + 2 * SZ_E * 4});
+    flush(b1);
+    exchange<2, 2>(sp, 1, L, X);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L[i] = R[i];
+    Bwd<2, 8, 2, true, true> a1{L, sc, T_EBLK + 16, lane};
+    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
+                                       Head<8, 2>{WE + 1 * SZ_E * 4});
+    flush(a1);
+    exchange<2, 2>(sp, 0, L, X);
+  }
+  const int E0T = Bk + OFF_E0 * 4 + wofs<16, 8>(w) / 2;   // local feature tiles 2w, 2w + 1
+  {
+    slice<2, 2>(X, w, R);
+    Bwd<2, 8, 2, false, true> b0{L, sc, T_EBLK, lane};
+    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 1 * SZ_E * 4, X, lane, b0, NoPre{},
+                                       Head<8, 2>{WE});
+    flush(b0);
+    exchange<2, 2>(sp, 1, L, X);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L[i] = R[i];
+    Bwd<2, 8, 2, true, true> a0{L, sc, T_E0, lane};
+    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE, X, lane, a0, NoPre{},
+                                       [=](int j, int l) {
+                                         return E0T + ((j / 8 + 8 * l) * 8 + j % 8) * 1024;
+                                       });
+    flush(a0);
+    exchange<2, 2>(sp, 0, L, X);
+  }
+
+  // ---- encoder[0]^T fused with the Fourier Jacobian (:639-645): this wave's feature tiles
+  // kf = 2w + kl (sin rows kf, cos rows kf + 8), then the dim-vector summed over the waves.
+  f32x4 ph[2][2][2];   // [kl][sin|cos rows][column]
+#pragma unroll
+  for (int kl = 0; kl < 2; ++kl)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) ph[kl][u][c] = zero4();
+  f32x4 bw[2][DIM];
+#pragma unroll
+  for (int kl = 0; kl < 2; ++kl)
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) bw[kl][d] = ld4(io.Bw + d * H + 16 * (2 * w + kl) + 4 * g);
+  run_steps<16, 2, NLA, SITE_FOLD>(
+      ring, W, lane * 16,
+      [&](int st, int l) { return E0T + ((st / 8 + 8 * l) * 8 + st % 8) * 1024; }, after,
+      [&](auto st, const f32x4 (&a)[2]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int kl = S / 8, kt = S % 8;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            ph[kl][0][c] = mfma(a[0][s], X[c * 8 + kt][s], ph[kl][0][c]);
+            ph[kl][1][c] = mfma(a[1][s], X[c * 8 + kt][s], ph[kl][1][c]);
+          }
+      });
+  float acc[2 * DIM];
+#pragma unroll
+  for (int j = 0; j < 2 * DIM; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int kl = 0; kl < 2; ++kl)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        float q = 0.f;
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], TWO_PI * bw[kl][d][s], q);
+        float sn, cs;
+        sincos_fast(q, sn, cs);
+        float gg = ph[kl][0][c][s] * cs - ph[kl][1][c][s] * sn;
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) acc[c * DIM + d] = fmaf(TWO_PI * bw[kl][d][s], gg, acc[c * DIM + d]);
+      }
+#pragma unroll
+  for (int j = 0; j < 2 * DIM; ++j) {
+    acc[j] += __shfl_xor(acc[j], 16);
+    acc[j] += __shfl_xor(acc[j], 32);
+  }
+  reduce_waves<2 * DIM>(sp, acc);
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) {
+    ds[d] = acc[d];
+    dg[d] = acc[DIM + d];
+  }
+}
+
+// Batched planner on split tiles: one workgroup per 16-query tile (grid-stride), the loop of
+// plan_kernel (test/gib_plan.py:74-86, test/arm_plan.py:140-152) with per-query freeze.
+// ws holds one scratch slot per wave (4 per workgroup).
+template <int DIM>
+__global__ __launch_bounds__(256, 1) void plan_split_kernel(PlanArgs a) {
+  __shared__ float smem[SPLIT_LDS_FLOATS];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Split sp{(lds_f*)smem, w, lane};
+  const int64_t ntiles = (a.q + TILE - 1) / TILE;
+  const Scratch sc = make_scratch(a.ws + ((int64_t)blockIdx.x * SPLIT + w) * SCRATCH_FLOATS_PER_WAVE);
+  const Rsrc W = make_rsrc(a.P, PACKED_FLOATS * 4);
+  const int cap = a.max_iter + 1;
+  const int64_t rows = (int64_t)cap + 1;
+  const SE0Head e0h = se0_head(w);
+  const Head<8> g3h{(OFF_BWD + OFF_G3) * 4 + wofs<16, 8>(w)};
+  Ring ring;
+  ring_fill<2>(ring, W, lane * 16, e0h);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    f32x4 X[16];
+    SplitCarry cy;
+    const int64_t qi = tile * TILE + (lane & 15);
+    PairIO io;
+    const bool ok = load_pair<DIM>(a.xp0, a.Btab, a.env, a.q, a.n_env, qi, io);
+    const bool store = w == 0 && (lane < 16) && qi < a.q;
+    float* prow = a.path + (store ? qi : 0) * rows * 2 * DIM;
+    auto dist = [&]() {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) {
+        float D = io.x[1][d] - io.x[0][d];
+        s = fmaf(D, D, s);
+      }
+      return sqrtf(s);
+    };
+    bool active = ok && dist() > a.tol;
+    if (store) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) prow[c * DIM + d] = io.x[c][d];
+    }
+    int nsteps = 0;
+    int it = 0;
+    for (; it < cap; ++it) {
+      if (!__any(active)) break;
+      float tau = split_forward<DIM, true, 4>(ring, a.P, io, X, cy, sc, a.compat, sp, g3h);
+      drain_stores();
+      float ds[DIM], dg[DIM], vs[DIM], vg[DIM];
+      split_backward<DIM, 2>(ring, a.P, io, tau, X, cy, sc, sp, ds, dg, e0h);
+      path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
+      if (active) {
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) {
+          io.x[0][d] = io.x[0][d] + a.step * vs[d];
+          io.x[1][d] = io.x[1][d] + a.step * vg[d];
+        }
+        ++nsteps;
+        if (!(dist() > a.tol)) active = false;
+      }
+      if (store) {
+        float* pr = prow + (int64_t)(it + 1) * 2 * DIM;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) pr[c * DIM + d] = io.x[c][d];
+      }
+    }
+    if (store) {
+      for (int64_t r = it + 1; r < rows; ++r) {
+        float* pr = prow + r * 2 * DIM;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) pr[c * DIM + d] = io.x[c][d];
+      }
+      a.steps[qi] = ok ? nsteps : -1;
+    }
+  }
+}
+
+}  // namespace pntf

@@ -43,6 +43,9 @@ SIGNATURES = {
     "pntf_plan": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
                                  _c_void_p, _i32, ctypes.c_int, _f32, _f32, _i32, _c_void_p,
                                  _c_void_p, _c_void_p, _size, _c_void_p]),
+    "pntf_plan_ex": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
+                                    _c_void_p, _i32, ctypes.c_int, _f32, _f32, _i32, _c_void_p,
+                                    _c_void_p, _c_void_p, _size, ctypes.c_int, _c_void_p]),
     "pntf_eikonal_residual": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _c_void_p,
                                              _i64, _c_void_p, _c_void_p, _i32, _f32,
                                              _c_void_p, _c_void_p, _c_void_p, _c_void_p,

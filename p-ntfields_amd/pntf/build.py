@@ -48,6 +48,8 @@ UNITS = (
     # spill-free (the 4-step ring spills 2 VGPRs there).
     + [("plan_d3", "pntf_kernels.hip", ["-DPNTF_DIM=3", "-DPNTF_PLAN"]),
        ("plan_d6", "pntf_kernels.hip", ["-DPNTF_DIM=6", "-DPNTF_PLAN", "-DPNTF_PF_STEPS=2"])]
+    + [("plan_split_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_SPLIT"])
+       for d in (3, 6)]
     + [("residual_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_RESIDUAL"])
        for d in (3, 6)]
     + [("util", "pntf_kernels.hip", ["-DPNTF_UTIL"]), ("capi", "pntf_capi.hip", [])]

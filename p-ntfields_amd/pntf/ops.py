@@ -154,21 +154,29 @@ def travel_time(packed, xp, Btab, env=None, dim=3):
     return tt
 
 
+SCHEDULES = {"auto": 0, "wave_tile": 1, "split_tile": 2}
+
+
 def plan(packed, xp0, Btab, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
-         mode=GRAD_BACKGRAD_COMPAT):
+         mode=GRAD_BACKGRAD_COMPAT, schedule="auto"):
     """Batched bidirectional planner (test/gib_plan.py:74-86; arm: test/arm_plan.py:140-152).
 
     Returns path (q, max_iter + 2, 2dim) — row 0 the start, frozen rows repeating the final
-    state — and steps (q,) int32 (updates taken per query)."""
+    state — and steps (q,) int32 (updates taken per query).  `schedule` picks the kernel
+    (include/pntf.h pntf_plan_ex): "wave_tile" (one wave per 16 queries), "split_tile" (four
+    waves share 16 queries: lower latency per step) or "auto"."""
+    if schedule not in SCHEDULES:
+        raise PntfError("unknown schedule %r" % (schedule,))
     lib = _lib.load()
     xp0, Bt, env = _prep(xp0, Btab, env, dim)
     q = xp0.shape[0]
     path = torch.empty((q, max_iter + 2, 2 * dim), dtype=torch.float32, device=xp0.device)
     steps = torch.empty(q, dtype=torch.int32, device=xp0.device)
     ws = _workspace(xp0.device, q)
-    check(lib.pntf_plan(_vp(packed), dim, _vp(xp0), q, _vp(Bt), _vp(env), Bt.shape[0], mode,
-                        float(step), float(tol), int(max_iter), _vp(path), _vp(steps), _vp(ws),
-                        ws.numel(), _stream(xp0.device)), "pntf_plan")
+    check(lib.pntf_plan_ex(_vp(packed), dim, _vp(xp0), q, _vp(Bt), _vp(env), Bt.shape[0],
+                           mode, float(step), float(tol), int(max_iter), _vp(path), _vp(steps),
+                           _vp(ws), ws.numel(), SCHEDULES[schedule], _stream(xp0.device)),
+          "pntf_plan_ex")
     return path, steps
 
 

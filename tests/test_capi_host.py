@@ -63,6 +63,11 @@ def test_argument_validation_without_gpu(lib):
                        None) == 0
     assert L.pntf_plan(None, 6, None, 4, None, None, 1, 0, 0.1, 0.1, -1, None, None, None, 0,
                        None) == 1
+    # unknown planner schedule, rejected before any device access
+    fake = ctypes.c_void_p(64)
+    assert L.pntf_plan_ex(fake, 6, fake, 4, fake, None, 1, 0, 0.1, 0.1, 5, fake, fake, fake,
+                          1 << 20, 7, None) == 1
+    assert b"schedule" in L.pntf_last_error()
 
 
 def test_no_cpu_fallback():

@@ -139,10 +139,12 @@ def test_coincident_endpoints(packed, dev, W):
     close(d.cpu().numpy(), do)
 
 
-def test_gibson_planner_vs_reference(packed, dev):
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile"])
+def test_gibson_planner_vs_reference(packed, dev, schedule):
     p = load("plan_gib.npz")
     path, steps = ops.plan(packed, T(p["starts"], dev), T(p["B"], dev), dim=3, step=0.03,
-                           tol=0.06, max_iter=500, mode=ops.GRAD_BACKGRAD_COMPAT)
+                           tol=0.06, max_iter=500, mode=ops.GRAD_BACKGRAD_COMPAT,
+                           schedule=schedule)
     path, steps = path.cpu().numpy(), steps.cpu().numpy()
     np.testing.assert_array_equal(steps, p["iters"])
     assert np.abs(path - p["paths"]).max() < 1e-3
@@ -151,24 +153,42 @@ def test_gibson_planner_vs_reference(packed, dev):
     assert np.abs(path[np.arange(len(steps)), steps] - last).max() < 1e-3
 
 
-def test_arm_planner_vs_reference(packed, dev):
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile"])
+def test_arm_planner_vs_reference(packed, dev, schedule):
     p = load("plan_arm.npz")
     path, steps = ops.plan(packed, T(p["starts"], dev), T(p["B"].T, dev), dim=6, step=0.015,
-                           tol=0.03, max_iter=300, mode=ops.GRAD_EXACT)
+                           tol=0.03, max_iter=300, mode=ops.GRAD_EXACT, schedule=schedule)
     path, steps = path.cpu().numpy(), steps.cpu().numpy()
     np.testing.assert_array_equal(steps, p["iters"])
     assert np.abs(path - p["paths"]).max() < 1e-3
 
 
-def test_planner_batch_vs_oracle(packed, dev, W):
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile"])
+def test_planner_batch_vs_oracle(packed, dev, schedule, W):
     q = 37
     xp0 = synth.make_box_pairs(q, 6, seed=77)
     B = synth.make_B(6, seed=12, arm=True).T.copy()
     path, steps = ops.plan(packed, T(xp0, dev), T(B, dev), dim=6, step=0.015, tol=0.03,
-                           max_iter=60, mode=ops.GRAD_EXACT)
+                           max_iter=60, mode=ops.GRAD_EXACT, schedule=schedule)
     po, so = O.plan(W, xp0, B, dim=6, step=0.015, tol=0.03, max_iter=60, compat=False)
     np.testing.assert_array_equal(steps.cpu().numpy(), so)
     assert np.abs(path.cpu().numpy() - po).max() < 1e-3
+
+
+@pytest.mark.parametrize("dim,compat", [(3, True), (6, False)])
+def test_planner_schedules_agree(packed, dev, dim, compat):
+    """Split tiles (4 waves per 16 queries, several tiles per workgroup at this q) against
+    one wave per tile: same iteration counts, paths equal to fp32 rounding."""
+    q = 16 * 600 + 5
+    xp0 = T(synth.make_box_pairs(q, dim, seed=91), dev)
+    B = synth.make_B(dim, seed=12, arm=dim == 6)
+    B = T(B.T.copy() if dim == 6 else B, dev)
+    kw = dict(dim=dim, step=0.03 if dim == 3 else 0.015, tol=0.06 if dim == 3 else 0.03,
+              max_iter=12, mode=ops.GRAD_BACKGRAD_COMPAT if compat else ops.GRAD_EXACT)
+    pw, sw = ops.plan(packed, xp0, B, schedule="wave_tile", **kw)
+    ps, ss = ops.plan(packed, xp0, B, schedule="split_tile", **kw)
+    assert torch.equal(sw, ss)
+    assert (ps - pw).abs().max().item() < 1e-4
 
 
 def test_drop_in_models_api(W, dev):

@@ -193,15 +193,22 @@ def extras(packed, dev):
     out["c2_tau_only_262144_pairs_per_s"] = n2 / (ms * 1e-3)
     ms = timeit(lambda: ops.path_velocity(packed, xp, B, dim=3))
     out["c2_path_velocity_262144_pairs_per_s"] = n2 / (ms * 1e-3)
+    # C1 shape on the GPU (4096 pairs, latency-bound): split tiles vs one wave per tile
+    x1 = torch.from_numpy(synth.make_pairs(4096, 3, seed=2)).to(dev)
+    for sched in ("auto", "wave_tile"):
+        ops.set_field_schedule(sched)
+        out["c1_tau_grad_4096_us_" + sched] = 1e3 * timeit(
+            lambda: ops.tau_grad(packed, x1, B, dim=3), reps=20)
+    ops.set_field_schedule("auto")
     # C3: Eikonal residual (Taylor mode + Model.Loss residual), 10 envs
-    n3 = 262144
+    n3 = 1 << 20
     x3 = torch.from_numpy(synth.make_pairs(n3, 3, seed=5)).to(dev)
     B3 = torch.from_numpy(synth.make_B_table(10, 3)).to(dev)
     e3 = torch.from_numpy(synth.make_env_ids(n3, 10)).to(dev)
     y3 = torch.from_numpy(synth.make_speeds(n3)).to(dev)
     ms = timeit(lambda: ops.eikonal_residual(packed, x3, B3, e3, 3, yobs=y3, gamma=1e-3),
                 reps=3)
-    out["c3_eikonal_residual_262144_pairs_per_s"] = n3 / (ms * 1e-3)
+    out["c3_eikonal_residual_1M_pairs_per_s"] = n3 / (ms * 1e-3)
     out["c3_eikonal_residual_TFLOPs"] = 14_286_848 * n3 / (ms * 1e-3) / 1e12
     # C5: UR5 arm, 1024 queries, <= 200 steps, per-query freeze
     q = 1024

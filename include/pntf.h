@@ -63,6 +63,11 @@ size_t pntf_packed_floats(void);
 int pntf_pack_weights(const float* const* params, int n_params, float* packed,
                       hipStream_t stream);
 
+/* Kernel schedule of pntf_tau / _tau_grad / _path_velocity / _speed / _travel_time
+ * (PNTF_SCHED_*, see pntf_plan_ex; AUTO by default).  Process-wide setting: not thread-safe
+ * against concurrent calls.  Results agree between schedules to fp32 rounding. */
+int pntf_set_field_schedule(int schedule);
+
 /* Device scratch needed by the gradient/planner entry points for n pairs. */
 size_t pntf_workspace_bytes(int64_t n);
 

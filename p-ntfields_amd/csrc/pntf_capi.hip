@@ -12,6 +12,8 @@
 namespace pntf {
 template <int DIM, int KIND>
 __global__ void field_kernel(FieldArgs a);
+template <int DIM, int KIND>
+__global__ void field_split_kernel(FieldArgs a);
 template <int DIM>
 __global__ void plan_kernel(PlanArgs a);
 template <int DIM>
@@ -76,6 +78,18 @@ static int grid_with_ws(int64_t n, size_t ws_bytes, int64_t* grid, bool split = 
   return PNTF_OK;
 }
 
+// Split tiles (pntf_split.h) while every tile still gets a CU of its own or shares one with
+// at most one other: a split tile takes ~1/3 of the one-wave time, and the one-wave kernels
+// win once the tiles fill every SIMD.
+static bool use_split(int64_t n, int schedule) {
+  if (schedule == PNTF_SCHED_SPLIT_TILE) return true;
+  if (schedule == PNTF_SCHED_WAVE_TILE) return false;
+  return (n + TILE - 1) / TILE <= 2 * (int64_t)num_cus();
+}
+
+// Schedule of the field entry points (pntf_set_field_schedule); process-wide.
+static int g_field_schedule = PNTF_SCHED_AUTO;
+
 // An empty batch is valid whatever the data pointers are (torch hands out NULL for empty
 // tensors); callers return PNTF_OK right after this check when n == 0.
 static int check_common(const float* packed, int dim, const float* xp, int64_t n,
@@ -89,8 +103,23 @@ static int check_common(const float* packed, int dim, const float* xp, int64_t n
 }
 
 template <int DIM>
-static void launch_field(int kind, int64_t grid, const FieldArgs& a, hipStream_t s) {
+static void launch_field(int kind, int64_t grid, const FieldArgs& a, hipStream_t s,
+                         bool split) {
   dim3 g((unsigned)grid), b(256);
+  if (split) {
+    switch (kind) {
+      case K_TAU: hipLaunchKernelGGL((field_split_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
+      case K_TAU_GRAD:
+        hipLaunchKernelGGL((field_split_kernel<DIM, K_TAU_GRAD>), g, b, 0, s, a);
+        break;
+      case K_VELOCITY:
+        hipLaunchKernelGGL((field_split_kernel<DIM, K_VELOCITY>), g, b, 0, s, a);
+        break;
+      case K_SPEED: hipLaunchKernelGGL((field_split_kernel<DIM, K_SPEED>), g, b, 0, s, a); break;
+      default: hipLaunchKernelGGL((field_split_kernel<DIM, K_TRAVEL>), g, b, 0, s, a); break;
+    }
+    return;
+  }
   switch (kind) {
     case K_TAU: hipLaunchKernelGGL((field_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
     case K_TAU_GRAD: hipLaunchKernelGGL((field_kernel<DIM, K_TAU_GRAD>), g, b, 0, s, a); break;
@@ -110,16 +139,17 @@ static int run_field(int kind, const float* packed, int dim, const float* xp, in
   if (n == 0) return PNTF_OK;
   if (!out0 || (kind == K_TAU_GRAD && !out1)) return fail(PNTF_ERR_ARG, "null output%s");
   const bool grad = kind != K_TAU && kind != K_TRAVEL;
-  int64_t grid = grid_for(n);
+  const bool split = use_split(n, g_field_schedule);
+  int64_t grid = split ? split_grid_for(n) : grid_for(n);
   if (grad) {
     if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
-    st = grid_with_ws(n, ws_bytes, &grid);
+    st = grid_with_ws(n, ws_bytes, &grid, split);
     if (st) return st;
   }
   FieldArgs a{packed, xp, Btab, env, n, n_env, mode, out0, out1, (float*)ws};
-  if (dim == 3) launch_field<3>(kind, grid, a, s);
-  else launch_field<6>(kind, grid, a, s);
-  return check_launch("field_kernel");
+  if (dim == 3) launch_field<3>(kind, grid, a, s, split);
+  else launch_field<6>(kind, grid, a, s, split);
+  return check_launch(split ? "field_split_kernel" : "field_kernel");
 }
 
 extern "C" {
@@ -139,6 +169,14 @@ const char* pntf_status_string(int status) {
 const char* pntf_last_error(void) { return g_err; }
 
 size_t pntf_packed_floats(void) { return (size_t)PACKED_FLOATS; }
+
+int pntf_set_field_schedule(int schedule) {
+  if (schedule != PNTF_SCHED_AUTO && schedule != PNTF_SCHED_WAVE_TILE &&
+      schedule != PNTF_SCHED_SPLIT_TILE)
+    return fail(PNTF_ERR_ARG, "unknown schedule%s");
+  g_field_schedule = schedule;
+  return PNTF_OK;
+}
 
 size_t pntf_workspace_bytes(int64_t n) {
   if (n <= 0) n = 1;
@@ -251,12 +289,7 @@ int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, cons
   if (q == 0) return PNTF_OK;
   if (!path || !steps) return fail(PNTF_ERR_ARG, "null output%s");
   if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
-  // Split tiles while every tile still gets a CU of its own or shares one with at most one
-  // other (a split step is ~3x faster than a one-wave step; the one-wave kernel wins once
-  // the tiles fill every SIMD).
-  const int64_t ntiles = (q + TILE - 1) / TILE;
-  const bool split = schedule == PNTF_SCHED_SPLIT_TILE ||
-                     (schedule == PNTF_SCHED_AUTO && ntiles <= 2 * (int64_t)num_cus());
+  const bool split = use_split(q, schedule);
   int64_t grid;
   st = grid_with_ws(q, ws_bytes, &grid, split);
   if (st) return st;

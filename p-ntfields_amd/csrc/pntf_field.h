@@ -893,6 +893,57 @@ __device__ __forceinline__ bool load_pair(const float* __restrict__ xp,
 }
 
 // ---------------------------------------------------------------- kernels
+// Per-kind outputs of one pair (lanes 0..15 store: `store`).
+template <int DIM, int KIND>
+__device__ __forceinline__ void store_field(const FieldArgs& a, int64_t pair, bool ok,
+                                            bool store, float tau, const PairIO& io,
+                                            const float (&ds)[DIM], const float (&dg)[DIM]) {
+  const float nan = __builtin_nanf("");
+  if (!ok) tau = nan;
+  if (KIND == K_TAU) {
+    if (store) a.out0[pair] = tau;
+  } else if (KIND == K_TRAVEL) {
+    float T0sq = 0.f;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
+      float D = io.x[1][d] - io.x[0][d];
+      T0sq = fmaf(D, D, T0sq);
+    }
+    if (store) a.out0[pair] = sqrtf(T0sq) / tau;
+  } else if (KIND == K_TAU_GRAD) {
+    if (store) {
+      a.out0[pair] = tau;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) {
+        a.out1[pair * 2 * DIM + d] = ok ? ds[d] : nan;
+        a.out1[pair * 2 * DIM + DIM + d] = ok ? dg[d] : nan;
+      }
+    }
+  } else if (KIND == K_VELOCITY) {
+    float vs[DIM], vg[DIM];
+    path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
+    if (store) {
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) {
+        a.out0[pair * 2 * DIM + d] = vs[d];
+        a.out0[pair * 2 * DIM + DIM + d] = vg[d];
+      }
+      if (a.out1) a.out1[pair] = tau;
+    }
+  } else {  // K_SPEED (Model.Speed, :1201-1213)
+    float T0 = 0.f, gg = 0.f, gD = 0.f;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
+      float D = io.x[1][d] - io.x[0][d];
+      T0 = fmaf(D, D, T0);
+      gg = fmaf(dg[d], dg[d], gg);
+      gD = fmaf(dg[d], D, gD);
+    }
+    float S = T0 * gg - 2.f * tau * gD + tau * tau;
+    if (store) a.out0[pair] = tau * tau / sqrtf(S);
+  }
+}
+
 // Persistent body: wave `slot` of `nslots` takes tiles slot, slot + nslots, ...
 template <int DIM, int KIND>
 __device__ __forceinline__ void field_body(const FieldArgs& a, int slot, int nslots) {
@@ -901,7 +952,6 @@ __device__ __forceinline__ void field_body(const FieldArgs& a, int slot, int nsl
   const int64_t ntiles = (a.n + TILE - 1) / TILE;
   const Scratch sc = make_scratch(GRAD ? a.ws + (int64_t)slot * SCRATCH_FLOATS_PER_WAVE : nullptr);
   const Rsrc W = make_rsrc(a.P, PACKED_FLOATS * 4);
-  const float nan = __builtin_nanf("");
   Ring ring;
   ring_fill<2>(ring, W, lane * 16, E0Head{});
   for (int64_t tile = slot; tile < ntiles; tile += nslots) {
@@ -918,53 +968,10 @@ __device__ __forceinline__ void field_body(const FieldArgs& a, int slot, int nsl
     if (GRAD) drain_stores();
     PNTF_STAMP(16);
     const bool store = (lane < 16) && pair < a.n;
-    if (!ok) tau = nan;
-    if (KIND == K_TAU) {
-      if (store) a.out0[pair] = tau;
-    } else if (KIND == K_TRAVEL) {
-      float T0sq = 0.f;
-#pragma unroll
-      for (int d = 0; d < DIM; ++d) {
-        float D = io.x[1][d] - io.x[0][d];
-        T0sq = fmaf(D, D, T0sq);
-      }
-      if (store) a.out0[pair] = sqrtf(T0sq) / tau;
-    } else {
-      float ds[DIM], dg[DIM];
+    float ds[DIM], dg[DIM];
+    if constexpr (GRAD)
       backward_pass<DIM, 2>(ring, a.P, io, tau, X, Y, cy, sc, lane, ds, dg, E0Head{});
-      if (KIND == K_TAU_GRAD) {
-        if (store) {
-          a.out0[pair] = tau;
-#pragma unroll
-          for (int d = 0; d < DIM; ++d) {
-            a.out1[pair * 2 * DIM + d] = ok ? ds[d] : nan;
-            a.out1[pair * 2 * DIM + DIM + d] = ok ? dg[d] : nan;
-          }
-        }
-      } else if (KIND == K_VELOCITY) {
-        float vs[DIM], vg[DIM];
-        path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
-        if (store) {
-#pragma unroll
-          for (int d = 0; d < DIM; ++d) {
-            a.out0[pair * 2 * DIM + d] = vs[d];
-            a.out0[pair * 2 * DIM + DIM + d] = vg[d];
-          }
-          if (a.out1) a.out1[pair] = tau;
-        }
-      } else {  // K_SPEED (Model.Speed, :1201-1213)
-        float T0 = 0.f, gg = 0.f, gD = 0.f;
-#pragma unroll
-        for (int d = 0; d < DIM; ++d) {
-          float D = io.x[1][d] - io.x[0][d];
-          T0 = fmaf(D, D, T0);
-          gg = fmaf(dg[d], dg[d], gg);
-          gD = fmaf(dg[d], D, gD);
-        }
-        float S = T0 * gg - 2.f * tau * gD + tau * tau;
-        if (store) a.out0[pair] = tau * tau / sqrtf(S);
-      }
-    }
+    store_field<DIM, KIND>(a, pair, ok, store, tau, io, ds, dg);
   }
 }
 

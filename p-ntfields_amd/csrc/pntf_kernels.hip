@@ -1,5 +1,6 @@
 // One kernel per translation unit, selected at build time (pntf/build.py):
 //   -DPNTF_KIND=0..4 -DPNTF_DIM=3|6   field_kernel<DIM, KIND>
+//   -DPNTF_KIND=0..4 -DPNTF_DIM=3|6 -DPNTF_SPLIT_FIELD   field_split_kernel<DIM, KIND>
 //   -DPNTF_PLAN -DPNTF_DIM=3|6         plan_kernel<DIM>
 //   -DPNTF_PLAN_SPLIT -DPNTF_DIM=3|6   plan_split_kernel<DIM> (pntf_split.h)
 //   -DPNTF_RESIDUAL -DPNTF_DIM=3|6     residual_kernel<DIM> (Taylor mode, pntf_taylor.h)
@@ -8,7 +9,9 @@
 #include "pntf_taylor.h"
 
 namespace pntf {
-#if defined(PNTF_KIND)
+#if defined(PNTF_KIND) && defined(PNTF_SPLIT_FIELD)
+template __global__ void field_split_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
+#elif defined(PNTF_KIND)
 template __global__ void field_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
 #elif defined(PNTF_PLAN)
 template __global__ void plan_kernel<PNTF_DIM>(PlanArgs);

@@ -477,6 +477,43 @@ __device__ __forceinline__ void split_backward(Ring& ring, const float* __restri
   }
 }
 
+// τ / ∇τ / epilogues on split tiles for small batches: one workgroup per 16-pair tile
+// (grid-stride), same outputs as field_kernel<DIM, KIND>.
+template <int DIM, int KIND>
+__global__ __launch_bounds__(256, 1) void field_split_kernel(FieldArgs a) {
+  constexpr bool GRAD = KIND != K_TAU && KIND != K_TRAVEL;
+  __shared__ float smem[SPLIT_LDS_FLOATS];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Split sp{(lds_f*)smem, w, lane};
+  const int64_t ntiles = (a.n + TILE - 1) / TILE;
+  const Scratch sc = make_scratch(
+      GRAD ? a.ws + ((int64_t)blockIdx.x * SPLIT + w) * SCRATCH_FLOATS_PER_WAVE : nullptr);
+  const Rsrc W = make_rsrc(a.P, PACKED_FLOATS * 4);
+  const SE0Head e0h = se0_head(w);
+  const Head<8> g3h{(OFF_BWD + OFF_G3) * 4 + wofs<16, 8>(w)};
+  Ring ring;
+  ring_fill<2>(ring, W, lane * 16, e0h);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    f32x4 X[16];
+    SplitCarry cy;
+    const int64_t pair = tile * TILE + (lane & 15);
+    PairIO io;
+    const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
+    float tau;
+    float ds[DIM], dg[DIM];
+    if constexpr (GRAD) {
+      tau = split_forward<DIM, true, 4>(ring, a.P, io, X, cy, sc, a.compat, sp, g3h);
+      drain_stores();
+      split_backward<DIM, 2>(ring, a.P, io, tau, X, cy, sc, sp, ds, dg, e0h);
+    } else {
+      tau = split_forward<DIM, false, 2>(ring, a.P, io, X, cy, sc, a.compat, sp, e0h);
+    }
+    const bool store = w == 0 && (lane < 16) && pair < a.n;
+    store_field<DIM, KIND>(a, pair, ok, store, tau, io, ds, dg);
+  }
+}
+
 // Batched planner on split tiles: one workgroup per 16-query tile (grid-stride), the loop of
 // plan_kernel (test/gib_plan.py:74-86, test/arm_plan.py:140-152) with per-query freeze.
 // ws holds one scratch slot per wave (4 per workgroup).

@@ -28,6 +28,7 @@ SIGNATURES = {
     "pntf_pack_weights": (ctypes.c_int, [ctypes.POINTER(_c_void_p), ctypes.c_int, _c_void_p,
                                          _c_void_p]),
     "pntf_workspace_bytes": (_size, [_i64]),
+    "pntf_set_field_schedule": (ctypes.c_int, [ctypes.c_int]),
     "pntf_tau": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p, _c_void_p,
                                 _i32, _c_void_p, _c_void_p]),
     "pntf_tau_grad": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,

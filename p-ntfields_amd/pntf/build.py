@@ -44,6 +44,9 @@ PACKED_FP32 = re.compile(r"\bv_pk_(mul|add|fma)_f32\b")
 UNITS = (
     [("field_d%d_k%d" % (d, k), "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k])
      for d in (3, 6) for k in range(5)]
+    + [("fsplit_d%d_k%d" % (d, k), "pntf_kernels.hip",
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_SPLIT_FIELD"])
+       for d in (3, 6) for k in range(5)]
     # plan_kernel<6> holds the 6-dof path state beside the ring: a 2-step ring keeps it
     # spill-free (the 4-step ring spills 2 VGPRs there).
     + [("plan_d3", "pntf_kernels.hip", ["-DPNTF_DIM=3", "-DPNTF_PLAN"]),

@@ -157,6 +157,15 @@ def travel_time(packed, xp, Btab, env=None, dim=3):
 SCHEDULES = {"auto": 0, "wave_tile": 1, "split_tile": 2}
 
 
+def set_field_schedule(schedule):
+    """Kernel schedule of tau / tau_grad / path_velocity / speed / travel_time
+    (include/pntf.h pntf_set_field_schedule): "auto" (default: split tiles for batches of at
+    most 2 x CUs x 16 pairs), "wave_tile" or "split_tile".  Process-wide."""
+    if schedule not in SCHEDULES:
+        raise PntfError("unknown schedule %r" % (schedule,))
+    check(_lib.load().pntf_set_field_schedule(SCHEDULES[schedule]), "pntf_set_field_schedule")
+
+
 def plan(packed, xp0, Btab, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
          mode=GRAD_BACKGRAD_COMPAT, schedule="auto"):
     """Batched bidirectional planner (test/gib_plan.py:74-86; arm: test/arm_plan.py:140-152).

@@ -68,6 +68,8 @@ def test_argument_validation_without_gpu(lib):
     assert L.pntf_plan_ex(fake, 6, fake, 4, fake, None, 1, 0, 0.1, 0.1, 5, fake, fake, fake,
                           1 << 20, 7, None) == 1
     assert b"schedule" in L.pntf_last_error()
+    assert L.pntf_set_field_schedule(7) == 1
+    assert L.pntf_set_field_schedule(0) == 0
 
 
 def test_no_cpu_fallback():

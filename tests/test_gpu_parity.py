@@ -42,11 +42,19 @@ def packed(W, dev):
     return ops.pack_weights(params)
 
 
+@pytest.fixture(params=["wave_tile", "split_tile"])
+def field_schedule(request):
+    """Run a field test with one wave per tile and with split tiles (pntf_split.h)."""
+    ops.set_field_schedule(request.param)
+    yield request.param
+    ops.set_field_schedule("auto")
+
+
 def T(a, dev, dtype=torch.float32):
     return torch.from_numpy(np.ascontiguousarray(a)).to(device=dev, dtype=dtype)
 
 
-def test_tau_grad_exact_vs_reference(packed, dev):
+def test_tau_grad_exact_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3, mode=ops.GRAD_EXACT)
     close(t.cpu().numpy(), f["tau"][:, 0])
@@ -54,13 +62,13 @@ def test_tau_grad_exact_vs_reference(packed, dev):
     close(d.cpu().numpy(), f["dtau_fwdmode"])
 
 
-def test_tau_only_kernel(packed, dev):
+def test_tau_only_kernel(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     t = ops.tau(packed, T(f["xp"], dev), T(f["B"], dev), dim=3)
     close(t.cpu().numpy(), f["tau"][:, 0])
 
 
-def test_backgrad_compat_vs_reference(packed, dev):
+def test_backgrad_compat_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3,
                         mode=ops.GRAD_BACKGRAD_COMPAT)
@@ -68,7 +76,7 @@ def test_backgrad_compat_vs_reference(packed, dev):
     close(d.cpu().numpy(), f["dtau_backgrad"])
 
 
-def test_epilogues_vs_reference(packed, dev):
+def test_epilogues_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     xp, B = T(f["xp"], dev), T(f["B"], dev)
     v, _ = ops.path_velocity(packed, xp, B, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT)
@@ -77,7 +85,7 @@ def test_epilogues_vs_reference(packed, dev):
     close(ops.travel_time(packed, xp, B, dim=3).cpu().numpy(), f["travel_time"])
 
 
-def test_env_table_vs_reference(packed, dev):
+def test_env_table_vs_reference(packed, dev, field_schedule):
     g = load("fwd_grad_env_d3.npz")
     xp, Bt, env = T(g["xp"], dev), T(g["B_table"], dev), T(g["env"], dev, torch.int32)
     t, d = ops.tau_grad(packed, xp, Bt, env, dim=3)
@@ -87,7 +95,7 @@ def test_env_table_vs_reference(packed, dev):
     close(dc.cpu().numpy(), g["dtau_backgrad"])
 
 
-def test_arm_dim6_vs_reference(packed, dev):
+def test_arm_dim6_vs_reference(packed, dev, field_schedule):
     a = load("fwd_grad_d6.npz")
     xp, B = T(a["xp"], dev), T(a["B"].T, dev)
     t, d = ops.tau_grad(packed, xp, B, dim=6)
@@ -98,7 +106,7 @@ def test_arm_dim6_vs_reference(packed, dev):
 
 
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 33, 1000, 4099])
-def test_ragged_batches_vs_oracle(packed, dev, W, n):
+def test_ragged_batches_vs_oracle(packed, dev, W, field_schedule, n):
     xp = synth.make_pairs(n, 3, seed=100 + n)
     Bt = synth.make_B_table(3, 3, first_seed=20)
     env = synth.make_env_ids(n, 3, contiguous=False, seed=n)
@@ -114,7 +122,7 @@ def test_empty_batch(packed, dev):
     assert t.shape == (0,) and d.shape == (0, 6)
 
 
-def test_invalid_env_gives_nan(packed, dev):
+def test_invalid_env_gives_nan(packed, dev, field_schedule):
     xp = synth.make_pairs(20, 3, seed=5)
     Bt = synth.make_B_table(2, 3)
     env = np.zeros(20, np.int32)

@@ -340,6 +340,174 @@ def eikonal_residual_arm(params, xp, yobs, B, dim=6, gamma=1e-3, dtype=np.float6
     return tau, dtau, ltau, diff
 
 
+# ------------------------------------------------------------------ training step (§8f rank 1)
+# Reverse mode through the Taylor-mode graph: what `loss.backward()` computes for the weights
+# in Model.train (model_res_sigmoid_multi.py:1040-1048; arm models/model_res_sigmoid.py:
+# 1062-1071).  Hand-derived adjoints of act_laplace (:675-691), linear_laplace (:663-673),
+# the merge (:761-811), actout_laplace (:693-708) and Model.Loss (:897-951).
+
+
+_BLOCK_HEADS = ("encoder.1", "encoder.2", "generator.0", "generator.1", "generator.2")
+
+
+def _tact_bwd(y, J, L, gh, gJ, gL):
+    """Adjoint of act_laplace: h = sp(y), J' = σJ, L' = σ'J² + σL, σ = σ(10y)."""
+    s = sig10(y)
+    ds = SCALE * s * (1.0 - s)
+    dds = SCALE * ds * (1.0 - 2.0 * s)
+    S, DS, DDS = s[:, None], ds[:, None], dds[:, None]
+    gy = gh * s + np.sum(gJ * J * DS + gL * (J * J * DDS + L * DS), axis=1)
+    return gy, gJ * S + 2.0 * gL * J * DS, gL * S
+
+
+def _tlin_bwd(x, J, L, W, gy, gJ, gL, grads, name):
+    """Adjoint of linear_laplace: the bias enters the value row only."""
+    grads[name + ".weight"] = grads.get(name + ".weight", 0) + (
+        gy.T @ x + np.einsum("nko,nki->oi", gJ, J) + np.einsum("nko,nki->oi", gL, L))
+    grads[name + ".bias"] = grads.get(name + ".bias", 0) + gy.sum(0)
+    return gy @ W, gJ @ W, gL @ W
+
+
+def _loss_bwd(xp, yobs, tau, dtau, ltau, dim, gamma, scale, arm):
+    """diff per pair and d(scale·Σdiff)/d(τ, ∇τ, Δτ rows) (Model.Loss :914-946; arm :869-935)."""
+    D = xp[:, dim:] - xp[:, :dim]
+    T0 = np.sum(D * D, 1)
+    t = tau[:, 0]
+    gt = np.zeros_like(t)
+    gd = np.zeros_like(dtau)
+    gl = np.zeros_like(ltau)
+    diff = -4.0
+    for k, sgn in ((0, 1.0), (1, -1.0)):
+        DT = dtau[:, k * dim:(k + 1) * dim]
+        lap = ltau[:, k * dim:(k + 1) * dim].sum(1)
+        dd = np.sum(DT * D, 1)
+        S = T0 * np.sum(DT * DT, 1) + sgn * 2.0 * t * dd + t * t
+        rS = np.sqrt(S)
+        Q = rS / (t * t) + gamma * lap
+        yp = 1.0 / Q
+        y = yobs[:, k]
+        if arm:
+            a, b = np.sqrt(yp), np.sqrt(y)
+            diff = diff + a / b + b / a
+            dfy = (1.0 / b - b / (a * a)) / (2.0 * a)
+        else:
+            diff = diff + yp / y + y / yp
+            dfy = 1.0 / y - y / (yp * yp)
+        gQ = -scale * dfy * yp * yp
+        gS = gQ / (2.0 * rS * t * t)
+        gt += gQ * (-2.0 * rS / (t * t * t)) + gS * (sgn * 2.0 * dd + 2.0 * t)
+        gd[:, k * dim:(k + 1) * dim] = gS[:, None] * (2.0 * T0[:, None] * DT + sgn * 2.0 * t[:, None] * D)
+        gl[:, k * dim:(k + 1) * dim] = (gQ * gamma)[:, None]
+    return diff, gt, gd, gl
+
+
+def eikonal_loss_grad(params, xp, yobs, B, env=None, dim=3, gamma=1e-3, scale=1.0, arm=False,
+                      dtype=np.float64):
+    """Weight gradients of scale·Σ_pairs diff — loss.backward() of Model.Loss with
+    scale = beta/(E·n) (multi, :947-948) or beta/N (arm).  The B regulariser of loss_n has no
+    weight gradient.  Returns (diff (N,), grads {state-dict key: array}); encoder1.0 gets none
+    (created :160 but never used)."""
+    p = cast_params(params, dtype)
+    xp = np.asarray(xp, dtype=dtype)
+    yobs = np.asarray(yobs, dtype=dtype)
+    n = xp.shape[0]
+    w, per = _per_point_W(B, env, n, dtype)
+    ww = np.concatenate([w, w]) if per else w
+    x = np.concatenate([xp[:, :dim], xp[:, dim:]])
+    q = _proj(x, ww, per)
+    sq, cq = np.sin(q), np.cos(q)
+    wd = ww if per else np.broadcast_to(w[None], (2 * n, dim, H))
+    phi = (np.concatenate([sq, cq], 1), np.concatenate([wd * cq[:, None], -wd * sq[:, None]], 2),
+           np.concatenate([-wd * wd * sq[:, None], -wd * wd * cq[:, None]], 2))
+    tape = []
+
+    def lin(t3, name, res=None):
+        out = _taylor_lin(*t3, p, name, res)
+        tape.append(("lin", name, t3, res is not None))
+        return out
+
+    def act(y3):
+        tape.append(("act", y3))
+        return _taylor_act(*y3)
+
+    h = act(lin(phi, "encoder.0"))
+    for i in (1, 2):
+        a = act(lin(h, "encoder.%d" % i))
+        h = act(lin(a, "encoder1.%d" % i, res=h))
+    z, Jz, Lz = lin(h, "encoder.3")
+    zs, zg, Js, Jg, Ls, Lg = z[:n], z[n:], Jz[:n], Jz[n:], Lz[:n], Lz[n:]
+    u, s0 = merge(zs, zg)
+    s1 = 1.0 - s0
+    c = SCALE * s0 * s1
+    S0, S1, C = s0[:, None], s1[:, None], c[:, None]
+    J = np.concatenate([np.concatenate([Js * S0, Js * S1], 2),
+                        np.concatenate([Jg * S1, Jg * S0], 2)], 1)
+    L = np.concatenate([np.concatenate([Js * C * Js + Ls * S0, -Js * C * Js + Ls * S1], 2),
+                        np.concatenate([Jg * C * Jg + Lg * S1, -Jg * C * Jg + Lg * S0], 2)], 1)
+    u3 = (u, J, L)
+    for i in (0, 1, 2):
+        a = act(lin(u3, "generator.%d" % i))
+        u3 = act(lin(a, "generator1.%d" % i, res=u3))
+    v3 = act(lin(u3, "generator.3"))
+    y, Jy, Ly = lin(v3, "generator.4")
+    y, Jy, Ly = y[:, 0], Jy[:, :, 0], Ly[:, :, 0]
+    t = sig_out(y)
+    dt = 0.1 * t * (1.0 - t)
+    ddt = 0.1 * dt * (1.0 - 2.0 * t)
+    dddt = 0.1 * (ddt * (1.0 - 2.0 * t) - 2.0 * dt * dt)
+    tau, dtau, ltau = t[:, None], Jy * dt[:, None], Jy * Jy * ddt[:, None] + Ly * dt[:, None]
+    diff, gt, gd, gl = _loss_bwd(xp, yobs, tau, dtau, ltau, dim, gamma, scale, arm)
+    # actout_laplace adjoint
+    g = (gt * dt + np.sum(gd * Jy * ddt[:, None] + gl * (Jy * Jy * dddt[:, None] + Ly * ddt[:, None]), 1),
+         gd * dt[:, None] + 2.0 * gl * Jy * ddt[:, None], gl * dt[:, None])
+    g = (g[0][:, None], g[1][:, :, None], g[2][:, :, None])
+    grads = {}
+    res_pending = []
+    gz = None
+    for op in reversed(tape):
+        if op[0] == "act":
+            g = _tact_bwd(*op[1], *g)
+            continue
+        _, name, x3, has_res = op
+        gin = _tlin_bwd(*x3, p[name + ".weight"], *g, grads, name)
+        if has_res:
+            res_pending.append(g)
+        if name in _BLOCK_HEADS:                   # the block input also feeds the residual
+            gin = tuple(a + b for a, b in zip(gin, res_pending.pop()))
+        g = gin
+        if name == "generator.0":
+            gu, gJ, gL = g
+            gM, gm = gu[:, :H], gu[:, H:]
+            gJsM, gJsm = gJ[:, :dim, :H], gJ[:, :dim, H:]
+            gJgM, gJgm = gJ[:, dim:, :H], gJ[:, dim:, H:]
+            gLsM, gLsm = gL[:, :dim, :H], gL[:, :dim, H:]
+            gLgM, gLgm = gL[:, dim:, :H], gL[:, dim:, H:]
+            g_s0 = np.sum((gJsM - gJsm) * Js - (gJgM - gJgm) * Jg
+                          + (gLsM - gLsm) * Ls - (gLgM - gLgm) * Lg, 1)
+            g_c = np.sum((gLsM - gLsm) * Js * Js + (gLgM - gLgm) * Jg * Jg, 1)
+            k = (g_s0 + g_c * SCALE * (1.0 - 2.0 * s0)) * c
+            gzs, gzg = gM * s0 + gm * s1 + k, gM * s1 + gm * s0 - k
+            gJs = gJsM * S0 + gJsm * S1 + 2.0 * C * Js * (gLsM - gLsm)
+            gJg = gJgM * S1 + gJgm * S0 + 2.0 * C * Jg * (gLgM - gLgm)
+            gLs, gLg = gLsM * S0 + gLsm * S1, gLgM * S1 + gLgm * S0
+            g = (np.concatenate([gzs, gzg]), np.concatenate([gJs, gJg]),
+                 np.concatenate([gLs, gLg]))
+    return diff, grads
+
+
+def adamw_step(param, grad, m, v, step, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, wd=0.1):
+    """torch.optim.AdamW single-tensor update (the reference's optimizer, :959-961); in place
+    on float64 copies; `step` is the 1-based step count after this update."""
+    param *= 1.0 - lr * wd
+    m += (1.0 - betas[0]) * (grad - m)
+    v *= betas[1]
+    v += (1.0 - betas[1]) * grad * grad
+    bc1 = 1.0 - betas[0] ** step
+    bc2 = 1.0 - betas[1] ** step
+    param -= (lr / bc1) * m / (np.sqrt(v) / np.sqrt(bc2) + eps)
+    return param
+
+
 def loss_n(diff, B_table, n_env, n_per_env):
     """loss_n (model_res_sigmoid_multi.py:947): sum(diff)/E/n + 0.01 ||B||^2 /E/n."""
     B = np.asarray(B_table, dtype=np.float64)

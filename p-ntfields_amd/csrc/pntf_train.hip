@@ -1,0 +1,531 @@
+// Training step of P-NTFields on MI355X: the weight gradient of the
+// Eikonal residual loss, i.e. what `loss.backward()` computes inside Model.train
+// (models/model_res_sigmoid_multi.py:1040-1052; arm models/model_res_sigmoid.py:1062-1075),
+// plus the AdamW update of the reference's optimizer (:959-961).
+//
+// Design ("Taylor tape"): the Taylor-mode forward of NN.out_laplace (:710-848)
+// is run layer by layer and every pre-activation is kept in HBM, then the reverse sweep
+// walks the tape back.  A Taylor tensor of M points and width W is stored as R = 1 + 2·ndir
+// planes (R, M, W): [value | ndir first-derivative rows | ndir diagonal second-derivative
+// rows] (ndir = dim in the encoder, 2·dim after the start/goal merge).  With that layout every
+// Linear of the graph is ONE plain fp32 GEMM over R·M rows (hipBLASLt, issued by the host),
+// the bias touching plane 0 only, and everything between the GEMMs is a fused elementwise
+// kernel here — one HBM pass per layer where the reference issues ~10 torch ops:
+//   tt_fourier_kernel   input_mapping_laplace (:199-213)           Φ planes
+//   tt_act_fwd_kernel   bias + act_laplace (:675-691)              y (saved), h planes
+//   tt_act_bwd_kernel   adjoint of act_laplace + bias gradient     g_y planes
+//   tt_merge_fwd/bwd    logsumexp merge of start/goal (:761-811) and its adjoint
+//   tt_head_loss_kernel generator[4] + actout_laplace (:693-708) + Model.Loss (:897-946)
+//                       forward AND backward per pair: diff, g of generator[3]'s output
+//   reduce_kernel       deterministic column sums of per-block partials (bias gradients)
+//   adamw_kernel        torch.optim.AdamW single-tensor update
+// All kernels are HBM-bound; they are written for coalesced 1-float-per-lane plane access
+// (consecutive lanes = consecutive features of one point) with grid-stride loops.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+
+#include "pntf.h"
+
+namespace {
+
+constexpr int H = 128;
+constexpr float SCALE = 10.f;               // Softplus beta (model_res_sigmoid_multi.py:140)
+constexpr float TWO_PI = 6.283185307179586f;
+constexpr int NB_MAX = 512;                 // partial-sum blocks of the reductions
+
+thread_local char g_err[512] = "";
+
+int fail(const char* what) {
+  snprintf(g_err, sizeof(g_err), "%s", what);
+  return PNTF_ERR_ARG;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return PNTF_ERR_HIP;
+  }
+  return PNTF_OK;
+}
+
+unsigned grid_1d(int64_t total, int64_t cap = 16384) {
+  int64_t g = (total + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+__device__ __forceinline__ float sig10(float y) { return 1.f / (1.f + expf(-SCALE * y)); }
+
+// torch.nn.Softplus(beta=10) with its default threshold 20 (linear above)
+__device__ __forceinline__ float softplus10(float y) {
+  return SCALE * y > 20.f ? y : log1pf(expf(SCALE * y)) / SCALE;
+}
+
+// ---------------------------------------------------------------- Φ planes (:199-213)
+// phi (1 + 2 DIM, 2n, 256): point m < n is x_start of pair m, m >= n the x_goal of pair m - n.
+template <int DIM>
+__global__ void tt_fourier_kernel(const float* __restrict__ xp, int64_t n,
+                                  const float* __restrict__ Btab, const int32_t* __restrict__ env,
+                                  int32_t n_env, float* __restrict__ phi) {
+  const int64_t M = 2 * n, plane = M * 256;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M * H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / H;
+    const int j = (int)(i % H);
+    const int64_t p = m < n ? m : m - n;
+    const float* x = xp + p * 2 * DIM + (m < n ? 0 : DIM);
+    const int e = env ? env[p] : 0;
+    float* o = phi + m * 256 + j;
+    if (e < 0 || e >= n_env) {
+      for (int r = 0; r < 1 + 2 * DIM; ++r) o[r * plane] = o[r * plane + H] = NAN;
+      continue;
+    }
+    const float* B = Btab + (int64_t)e * DIM * H + j;
+    float w[DIM], q = 0.f;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) {
+      w[k] = TWO_PI * B[k * H];
+      q = fmaf(x[k], w[k], q);
+    }
+    float s, c;
+    sincosf(q, &s, &c);
+    o[0] = s;
+    o[H] = c;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) {
+      o[(1 + k) * plane] = w[k] * c;
+      o[(1 + k) * plane + H] = -w[k] * s;
+      o[(1 + DIM + k) * plane] = -w[k] * w[k] * s;
+      o[(1 + DIM + k) * plane + H] = -w[k] * w[k] * c;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- act_laplace (:675-691)
+// y (R, M, W): GEMM output; plane 0 gets the bias (kept in place as the saved
+// pre-activation).  ACT: h = softplus10(y), J' = σJ, L' = σ'J² + σL (σ = σ(10y), σ' = 10σ(1-σ)).
+template <int NDIR, bool ACT>
+__global__ void tt_act_fwd_kernel(float* __restrict__ y, float* __restrict__ h,
+                                  const float* __restrict__ bias, int64_t M, int W) {
+  const int64_t plane = M * W;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < plane;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = y[i] + bias[i % W];
+    y[i] = v;
+    if (!ACT) continue;
+    const float s = sig10(v), ds = SCALE * s * (1.f - s);
+    h[i] = softplus10(v);
+#pragma unroll
+    for (int k = 0; k < NDIR; ++k) {
+      const float J = y[(1 + k) * plane + i], L = y[(1 + NDIR + k) * plane + i];
+      h[(1 + k) * plane + i] = J * s;
+      h[(1 + NDIR + k) * plane + i] = fmaf(J * J, ds, L * s);
+    }
+  }
+}
+
+// Per-block column partial sums of a (rows, W) value -> partial[blockIdx][W]: the thread owns
+// column tid % W and rows tid / W + k·RB; the RB row groups are folded through LDS.
+template <int W>
+__device__ __forceinline__ void block_colsum(float acc, float* __restrict__ partial) {
+  constexpr int RB = 256 / W;
+  __shared__ float red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < W) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) s += red[r * W + threadIdx.x];
+    partial[blockIdx.x * W + threadIdx.x] = s;
+  }
+}
+
+// Adjoint of act_laplace, in place on g (dL/dh planes in, dL/dy planes out):
+//   g_y = g_h σ + Σ_k g_Jk J_k σ' + g_Lk (J_k² σ'' + L_k σ')    σ'' = 10 σ' (1 - 2σ)
+//   g_J = g_J σ + 2 g_L J σ'      g_L = g_L σ
+// ACT=false (a Linear with no activation) only forms the bias partials.
+template <int NDIR, int W, bool ACT>
+__global__ __launch_bounds__(256) void tt_act_bwd_kernel(const float* __restrict__ y,
+                                                         float* __restrict__ g, int64_t M,
+                                                         float* __restrict__ partial) {
+  constexpr int RB = 256 / W;
+  const int64_t plane = M * W;
+  const int j = threadIdx.x % W;
+  float acc = 0.f;
+  for (int64_t m = blockIdx.x * RB + threadIdx.x / W; m < M; m += (int64_t)gridDim.x * RB) {
+    const int64_t i = m * W + j;
+    if (!ACT) {
+      acc += g[i];
+      continue;
+    }
+    const float v = y[i];
+    const float s = sig10(v), ds = SCALE * s * (1.f - s), dds = SCALE * ds * (1.f - 2.f * s);
+    float gy = g[i] * s;
+#pragma unroll
+    for (int k = 0; k < NDIR; ++k) {
+      const int64_t iJ = (1 + k) * plane + i, iL = (1 + NDIR + k) * plane + i;
+      const float J = y[iJ], L = y[iL], gJ = g[iJ], gL = g[iL];
+      gy += gJ * J * ds + gL * fmaf(J * J, dds, L * ds);
+      g[iJ] = fmaf(gJ, s, 2.f * gL * J * ds);
+      g[iL] = gL * s;
+    }
+    g[i] = gy;
+    acc += gy;
+  }
+  block_colsum<W>(acc, partial);
+}
+
+// out[j] (+)= Σ_b partial[b][j] in block order (deterministic)
+__global__ void reduce_kernel(const float* __restrict__ partial, int nb, int W,
+                              float* __restrict__ out, int accumulate) {
+  for (int j = threadIdx.x; j < W; j += blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < nb; ++b) s += partial[b * W + j];
+    out[j] = accumulate ? out[j] + s : s;
+  }
+}
+
+// ---------------------------------------------------------------- start/goal merge (:761-811)
+// z (1 + 2 DIM, 2n, 128) encoder output planes -> u (1 + 4 DIM, n, 256) generator planes
+// [value | ∂xs (DIM) | ∂xg (DIM) | ∂²xs (DIM) | ∂²xg (DIM)], features [max-part | min-part].
+template <int DIM>
+__global__ void tt_merge_fwd_kernel(const float* __restrict__ z, int64_t n,
+                                    float* __restrict__ u) {
+  const int64_t pz = 2 * n * H, pu = n * 256;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / H;
+    const int j = (int)(i % H);
+    const int64_t is = p * H + j, ig = (n + p) * H + j, o = p * 256 + j;
+    const float zs = z[is], zg = z[ig], d = zs - zg;
+    const float lse = log1pf(expf(-SCALE * fabsf(d))) / SCALE;
+    u[o] = fmaxf(zs, zg) + lse;
+    u[o + H] = fminf(zs, zg) - lse;
+    const float s0 = sig10(d), s1 = 1.f - s0, c = SCALE * s0 * s1;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) {
+      const float Js = z[(1 + k) * pz + is], Jg = z[(1 + k) * pz + ig];
+      const float Ls = z[(1 + DIM + k) * pz + is], Lg = z[(1 + DIM + k) * pz + ig];
+      u[(1 + k) * pu + o] = Js * s0;
+      u[(1 + k) * pu + o + H] = Js * s1;
+      u[(1 + DIM + k) * pu + o] = Jg * s1;
+      u[(1 + DIM + k) * pu + o + H] = Jg * s0;
+      const float cs = c * Js * Js, cg = c * Jg * Jg;
+      u[(1 + 2 * DIM + k) * pu + o] = cs + Ls * s0;
+      u[(1 + 2 * DIM + k) * pu + o + H] = -cs + Ls * s1;
+      u[(1 + 3 * DIM + k) * pu + o] = cg + Lg * s1;
+      u[(1 + 3 * DIM + k) * pu + o + H] = -cg + Lg * s0;
+    }
+  }
+}
+
+// Adjoint of the merge: gu (1 + 4 DIM, n, 256) -> gz (1 + 2 DIM, 2n, 128).
+template <int DIM>
+__global__ void tt_merge_bwd_kernel(const float* __restrict__ z, const float* __restrict__ gu,
+                                    int64_t n, float* __restrict__ gz) {
+  const int64_t pz = 2 * n * H, pu = n * 256;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / H;
+    const int j = (int)(i % H);
+    const int64_t is = p * H + j, ig = (n + p) * H + j, o = p * 256 + j;
+    const float d = z[is] - z[ig];
+    const float s0 = sig10(d), s1 = 1.f - s0, c = SCALE * s0 * s1;
+    float g_s0 = 0.f, g_c = 0.f;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) {
+      const float Js = z[(1 + k) * pz + is], Jg = z[(1 + k) * pz + ig];
+      const float Ls = z[(1 + DIM + k) * pz + is], Lg = z[(1 + DIM + k) * pz + ig];
+      const float gJsM = gu[(1 + k) * pu + o], gJsm = gu[(1 + k) * pu + o + H];
+      const float gJgM = gu[(1 + DIM + k) * pu + o], gJgm = gu[(1 + DIM + k) * pu + o + H];
+      const float gLsM = gu[(1 + 2 * DIM + k) * pu + o];
+      const float gLsm = gu[(1 + 2 * DIM + k) * pu + o + H];
+      const float gLgM = gu[(1 + 3 * DIM + k) * pu + o];
+      const float gLgm = gu[(1 + 3 * DIM + k) * pu + o + H];
+      const float dLs = gLsM - gLsm, dLg = gLgM - gLgm;
+      g_s0 += (gJsM - gJsm) * Js - (gJgM - gJgm) * Jg + dLs * Ls - dLg * Lg;
+      g_c += dLs * Js * Js + dLg * Jg * Jg;
+      gz[(1 + k) * pz + is] = gJsM * s0 + gJsm * s1 + 2.f * c * Js * dLs;
+      gz[(1 + k) * pz + ig] = gJgM * s1 + gJgm * s0 + 2.f * c * Jg * dLg;
+      gz[(1 + DIM + k) * pz + is] = gLsM * s0 + gLsm * s1;
+      gz[(1 + DIM + k) * pz + ig] = gLgM * s1 + gLgm * s0;
+    }
+    const float kk = (g_s0 + g_c * SCALE * (1.f - 2.f * s0)) * c;
+    const float gM = gu[o], gm = gu[o + H];
+    gz[is] = gM * s0 + gm * s1 + kk;
+    gz[ig] = gM * s1 + gm * s0 - kk;
+  }
+}
+
+// ---------------------------------------------------------------- head + loss, fwd and bwd
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// One wave per pair.  v (R, n, 128) = generator[3]'s Taylor output, R = 1 + 4 DIM.
+// Forward: y_r = w4·v_r (+ b4 on r = 0); τ = σ(0.1 y), ∇τ, Δτ rows (actout_laplace :693-708);
+// diff (Model.Loss :914-946, ARM: models/model_res_sigmoid.py:888-933).  Backward of
+// scale·Σ diff: g_r per row, written as gv_r = g_r w4 (the input gradient of generator[4])
+// and folded into per-block partials of g_w4 = Σ g_r v_r and g_b4 = Σ g_0.
+template <int DIM, bool ARM>
+__global__ __launch_bounds__(256) void tt_head_loss_kernel(
+    const float* __restrict__ v, const float* __restrict__ w4, const float* __restrict__ b4,
+    const float* __restrict__ xp, const float* __restrict__ yobs, int64_t n, float gamma,
+    float scale, float* __restrict__ diff, float* __restrict__ gv, float* __restrict__ partial) {
+  constexpr int R = 1 + 4 * DIM, ND = 2 * DIM;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t plane = n * H;
+  const float wa = w4[lane], wb = w4[lane + 64], bias = b4[0];
+  float gwa = 0.f, gwb = 0.f, gb = 0.f;
+  for (int64_t p = blockIdx.x * 4 + wave; p < n; p += (int64_t)gridDim.x * 4) {
+    float yr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float* row = v + r * plane + p * H;
+      yr[r] = wave_sum(fmaf(row[lane], wa, row[lane + 64] * wb));
+    }
+    const float y = yr[0] + bias;
+    const float t = 1.f / (1.f + expf(-0.1f * y));
+    const float dt = 0.1f * t * (1.f - t), ddt = 0.1f * dt * (1.f - 2.f * t);
+    const float dddt = 0.1f * (ddt * (1.f - 2.f * t) - 2.f * dt * dt);
+    float dtau[ND], ltau[ND];
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      const float J = yr[1 + k], L = yr[1 + ND + k];
+      dtau[k] = J * dt;
+      ltau[k] = fmaf(J * J, ddt, L * dt);
+    }
+    // ---- Model.Loss and its adjoint
+    const float* x = xp + p * 2 * DIM;
+    float D[DIM], T0 = 0.f;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) {
+      D[k] = x[DIM + k] - x[k];
+      T0 = fmaf(D[k], D[k], T0);
+    }
+    float gt = 0.f, gd[ND], gl[2], df = -4.f;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float sgn = e == 0 ? 1.f : -1.f;
+      float dd = 0.f, nn = 0.f, lap = 0.f;
+#pragma unroll
+      for (int k = 0; k < DIM; ++k) {
+        dd = fmaf(dtau[e * DIM + k], D[k], dd);
+        nn = fmaf(dtau[e * DIM + k], dtau[e * DIM + k], nn);
+        lap += ltau[e * DIM + k];
+      }
+      const float S = T0 * nn + sgn * 2.f * t * dd + t * t;
+      const float rS = sqrtf(S);
+      const float yp = 1.f / (rS / (t * t) + gamma * lap);
+      const float yo = yobs[p * 2 + e];
+      float dfy;
+      if (ARM) {
+        const float a = sqrtf(yp), b = sqrtf(yo);
+        df += a / b + b / a;
+        dfy = (1.f / b - b / (a * a)) / (2.f * a);
+      } else {
+        df += yp / yo + yo / yp;
+        dfy = 1.f / yo - yo / (yp * yp);
+      }
+      const float gQ = -scale * dfy * yp * yp;
+      const float gS = gQ / (2.f * rS * t * t);
+      gt += gQ * (-2.f * rS / (t * t * t)) + gS * (sgn * 2.f * dd + 2.f * t);
+#pragma unroll
+      for (int k = 0; k < DIM; ++k)
+        gd[e * DIM + k] = gS * (2.f * T0 * dtau[e * DIM + k] + sgn * 2.f * t * D[k]);
+      gl[e] = gQ * gamma;
+    }
+    if (lane == 0) diff[p] = df;
+    // ---- actout_laplace adjoint -> g_r of generator[4]'s output rows
+    float g0 = gt * dt;
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      const float J = yr[1 + k], L = yr[1 + ND + k], gL = gl[k / DIM];
+      g0 += gd[k] * J * ddt + gL * fmaf(J * J, dddt, L * ddt);
+    }
+    gb += g0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float g;
+      if (r == 0) g = g0;
+      else if (r <= ND) g = gd[r - 1] * dt + 2.f * gl[(r - 1) / DIM] * yr[r] * ddt;
+      else g = gl[(r - 1 - ND) / DIM] * dt;
+      const float* row = v + r * plane + p * H;
+      float* grow = gv + r * plane + p * H;
+      gwa = fmaf(g, row[lane], gwa);
+      gwb = fmaf(g, row[lane + 64], gwb);
+      grow[lane] = g * wa;
+      grow[lane + 64] = g * wb;
+    }
+  }
+  // per-block partials: [gridDim][128] for g_w4, then [gridDim] for g_b4
+  __shared__ float red[4][129];
+  red[wave][lane] = gwa;
+  red[wave][lane + 64] = gwb;
+  if (lane == 0) red[wave][128] = gb;
+  __syncthreads();
+  if (threadIdx.x < 129) {
+    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                    red[3][threadIdx.x];
+    if (threadIdx.x < 128) partial[blockIdx.x * 128 + threadIdx.x] = s;
+    else partial[(int64_t)gridDim.x * 128 + blockIdx.x] = s;
+  }
+}
+
+// ---------------------------------------------------------------- AdamW (torch.optim.AdamW)
+// Same operation order as torch's single-tensor AdamW: p *= 1 - lr·wd; m = lerp(m, g, 1-β1);
+// v = β2 v + (1-β2) g²; p -= step_size · m / (sqrt(v)/sqrt(bc2) + eps).
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v, int64_t n,
+                             float decay, float one_minus_b1, float b2, float one_minus_b2,
+                             float step_size, float bc2_sqrt, float eps) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = fmaf(one_minus_b1, gi - mi, mi);
+    const float vi = fmaf(b2, v[i], one_minus_b2 * gi * gi);
+    pi -= step_size * mi / (sqrtf(vi) / bc2_sqrt + eps);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+int nb_for(int64_t rows) {
+  int64_t nb = rows < 1 ? 1 : rows;
+  return (int)(nb > NB_MAX ? NB_MAX : nb);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t pntf_tt_partial_floats(void) { return (size_t)NB_MAX * 257; }
+
+const char* pntf_tt_last_error(void) { return g_err; }
+
+int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, const int32_t* env,
+                    int32_t n_env, float* phi, hipStream_t stream) {
+  if ((dim != 3 && dim != 6) || n < 0 || n_env < 1 || (n > 0 && (!xp || !Btab || !phi)))
+    return fail("pntf_tt_fourier: bad arguments");
+  if (n == 0) return PNTF_OK;
+  const unsigned g = grid_1d(2 * n * H);
+  if (dim == 3)
+    hipLaunchKernelGGL((tt_fourier_kernel<3>), dim3(g), dim3(256), 0, stream, xp, n, Btab, env,
+                       n_env, phi);
+  else
+    hipLaunchKernelGGL((tt_fourier_kernel<6>), dim3(g), dim3(256), 0, stream, xp, n, Btab, env,
+                       n_env, phi);
+  return check_launch("tt_fourier_kernel");
+}
+
+int pntf_tt_act_fwd(int ndir, float* y, float* h, const float* bias, int64_t m, int w, int act,
+                    hipStream_t stream) {
+  if ((ndir != 3 && ndir != 6 && ndir != 12) || m < 0 || (w != 128 && w != 256) ||
+      (m > 0 && (!y || !bias || (act && !h))))
+    return fail("pntf_tt_act_fwd: bad arguments");
+  if (m == 0) return PNTF_OK;
+  const dim3 g(grid_1d(m * w)), b(256);
+#define PNTF_ACT_FWD(N)                                                                   \
+  if (act) hipLaunchKernelGGL((tt_act_fwd_kernel<N, true>), g, b, 0, stream, y, h, bias, m, w); \
+  else hipLaunchKernelGGL((tt_act_fwd_kernel<N, false>), g, b, 0, stream, y, h, bias, m, w);
+  if (ndir == 3) { PNTF_ACT_FWD(3) }
+  else if (ndir == 6) { PNTF_ACT_FWD(6) }
+  else { PNTF_ACT_FWD(12) }
+#undef PNTF_ACT_FWD
+  return check_launch("tt_act_fwd_kernel");
+}
+
+int pntf_tt_act_bwd(int ndir, const float* y, float* g, int64_t m, int w, int act, float* gbias,
+                    int accumulate, float* partial, hipStream_t stream) {
+  if ((ndir != 3 && ndir != 6 && ndir != 12) || m < 0 || (w != 128 && w != 256) || !gbias ||
+      !partial || (m > 0 && (!g || (act && !y))))
+    return fail("pntf_tt_act_bwd: bad arguments");
+  const int nb = nb_for(m / (256 / w));
+  const dim3 gr(nb), b(256);
+#define PNTF_ACT_BWD(N, W)                                                                 \
+  if (act) hipLaunchKernelGGL((tt_act_bwd_kernel<N, W, true>), gr, b, 0, stream, y, g, m,     \
+                              partial);                                                     \
+  else hipLaunchKernelGGL((tt_act_bwd_kernel<N, W, false>), gr, b, 0, stream, y, g, m, partial);
+  if (w == 128) {
+    if (ndir == 3) { PNTF_ACT_BWD(3, 128) }
+    else if (ndir == 6) { PNTF_ACT_BWD(6, 128) }
+    else { PNTF_ACT_BWD(12, 128) }
+  } else {
+    if (ndir == 3) { PNTF_ACT_BWD(3, 256) }
+    else if (ndir == 6) { PNTF_ACT_BWD(6, 256) }
+    else { PNTF_ACT_BWD(12, 256) }
+  }
+#undef PNTF_ACT_BWD
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, stream, partial, nb, w, gbias,
+                     accumulate);
+  return check_launch("tt_act_bwd_kernel");
+}
+
+int pntf_tt_merge_fwd(int dim, const float* z, int64_t n, float* u, hipStream_t stream) {
+  if ((dim != 3 && dim != 6) || n < 0 || (n > 0 && (!z || !u)))
+    return fail("pntf_tt_merge_fwd: bad arguments");
+  if (n == 0) return PNTF_OK;
+  const dim3 g(grid_1d(n * H)), b(256);
+  if (dim == 3) hipLaunchKernelGGL((tt_merge_fwd_kernel<3>), g, b, 0, stream, z, n, u);
+  else hipLaunchKernelGGL((tt_merge_fwd_kernel<6>), g, b, 0, stream, z, n, u);
+  return check_launch("tt_merge_fwd_kernel");
+}
+
+int pntf_tt_merge_bwd(int dim, const float* z, const float* gu, int64_t n, float* gz,
+                      hipStream_t stream) {
+  if ((dim != 3 && dim != 6) || n < 0 || (n > 0 && (!z || !gu || !gz)))
+    return fail("pntf_tt_merge_bwd: bad arguments");
+  if (n == 0) return PNTF_OK;
+  const dim3 g(grid_1d(n * H)), b(256);
+  if (dim == 3) hipLaunchKernelGGL((tt_merge_bwd_kernel<3>), g, b, 0, stream, z, gu, n, gz);
+  else hipLaunchKernelGGL((tt_merge_bwd_kernel<6>), g, b, 0, stream, z, gu, n, gz);
+  return check_launch("tt_merge_bwd_kernel");
+}
+
+int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const float* b4,
+                      const float* xp, const float* yobs, int64_t n, float gamma, float scale,
+                      float* diff, float* gv, float* gw4, float* gb4, float* partial,
+                      hipStream_t stream) {
+  if ((dim != 3 && dim != 6) || n < 0 || !w4 || !b4 || !gw4 || !gb4 || !partial ||
+      (n > 0 && (!v || !xp || !yobs || !diff || !gv)))
+    return fail("pntf_tt_head_loss: bad arguments");
+  const int nb = nb_for((n + 3) / 4);
+  const dim3 g(nb), b(256);
+#define PNTF_HEAD(D, A)                                                                     \
+  hipLaunchKernelGGL((tt_head_loss_kernel<D, A>), g, b, 0, stream, v, w4, b4, xp, yobs, n,   \
+                     gamma, scale, diff, gv, partial)
+  if (dim == 3) {
+    if (arm) PNTF_HEAD(3, true);
+    else PNTF_HEAD(3, false);
+  } else {
+    if (arm) PNTF_HEAD(6, true);
+    else PNTF_HEAD(6, false);
+  }
+#undef PNTF_HEAD
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, stream, partial, nb, 128, gw4, 0);
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(64), 0, stream, partial + (int64_t)nb * 128,
+                     nb, 1, gb4, 0);
+  return check_launch("tt_head_loss_kernel");
+}
+
+int pntf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+               float beta2, float eps, float weight_decay, int64_t step, hipStream_t stream) {
+  if (n < 0 || step < 1 || (n > 0 && (!p || !g || !m || !v)))
+    return fail("pntf_adamw: bad arguments");
+  if (n == 0) return PNTF_OK;
+  // host-side scalars in double, as torch computes them in Python floats
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_1d(n, 4096)), dim3(256), 0, stream, p, g, m, v, n,
+                     (float)(1.0 - (double)lr * weight_decay), (float)(1.0 - beta1), beta2,
+                     (float)(1.0 - beta2), (float)(lr / bc1), (float)sqrt(bc2), eps);
+  return check_launch("adamw_kernel");
+}
+
+}  // extern "C"

@@ -11,6 +11,7 @@ import numpy as np
 import torch
 
 from pntf import ops
+from pntf import train as _train
 from pntf.net import PackedCache, TauFunction, build_layers
 from pntf.net import init_weights as _init_weights
 
@@ -91,8 +92,15 @@ class Model:
 
     def Loss(self, points, Yobs, beta, gamma):
         """The arm variant of the residual (models/model_res_sigmoid.py:869-935: square-root
-        speeds, viscosity on 1/Ypred).  τ, ∇τ and ∇²τ come from the HIP Taylor kernel; the
-        few elementwise epilogue ops run as device tensor ops.  Values only."""
+        speeds, viscosity on 1/Ypred).  Training (grad enabled, trainable weights): the HIP
+        Taylor-tape adjoint (pntf/train.py), `loss.backward()` fills the weights' .grad.
+        Otherwise τ, ∇τ and ∇²τ come from the fused HIP Taylor kernel and the few
+        elementwise epilogue ops run as device tensor ops (values only)."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.network.parameters()):
+            Bt = self.network._B(points.device).reshape(1, self.dim, -1)
+            total, diff = _train.eikonal_loss(self.network, points, Yobs, Bt, None, self.dim,
+                                              gamma, 1.0 / points.shape[0], arm=True)
+            return beta * total, total, diff
         tau, dtau, ltau, Xp = self.network.out_laplace(points)
         d = self.dim
         D = Xp[:, d:] - Xp[:, :d]

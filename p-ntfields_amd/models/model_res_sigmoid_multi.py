@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from pntf import ops
+from pntf import train as _train
 from pntf.net import PackedCache, TauFunction, build_layers
 from pntf.net import init_weights as _init_weights
 
@@ -169,16 +170,26 @@ class Model:
 
     def Loss(self, points, Yobs, B, beta, gamma):
         """Eikonal residual loss (:897-951): points (E,n,2dim), Yobs (E,n,2), B (E,dim,128).
-        Returns (loss, loss_n, diff (E,n)); the per-pair residual and its sum run on the
-        HIP kernels.  Values only: the weight gradient (training) is not on this path."""
+        Returns (loss, loss_n, diff (E,n)).  With grad enabled and trainable weights (the
+        training step, :1040-1048) `loss.backward()` fills the weights' .grad through the HIP
+        Taylor-tape adjoint (pntf/train.py); otherwise the fused residual kernel evaluates
+        the values only."""
         E, n, _ = points.shape
         dev = points.device
         Bt = _as_table(B, dev)
+        reg = 0.01 * ops.device_sum(Bt * Bt).float() / E / n
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.network.parameters()):
+            total, diff = _train.eikonal_loss(self.network, points.reshape(E * n, -1),
+                                              Yobs.reshape(E * n, 2), Bt,
+                                              _env_ids(E, n, dev), self.dim, gamma,
+                                              1.0 / (E * n))
+            loss_n = total + reg
+            return beta * loss_n, loss_n, diff.view(E, n)
         out = ops.eikonal_residual(self.network.packed(), points.reshape(E * n, -1), Bt,
                                    _env_ids(E, n, dev), self.dim,
                                    yobs=Yobs.reshape(E * n, 2), gamma=gamma, want=("diff",))
         diff = out["diff"].view(E, n)
-        loss_n = (ops.device_sum(diff) / E / n + 0.01 * ops.device_sum(Bt * Bt) / E / n).float()
+        loss_n = (ops.device_sum(diff) / E / n).float() + reg
         return beta * loss_n, loss_n, diff
 
     def train(self):

@@ -52,6 +52,25 @@ SIGNATURES = {
                                              _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                              _c_void_p, _size, _c_void_p]),
     "pntf_sum": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    # training step (pntf_train.hip)
+    "pntf_tt_partial_floats": (_size, []),
+    "pntf_tt_last_error": (ctypes.c_char_p, []),
+    "pntf_tt_fourier": (ctypes.c_int, [ctypes.c_int, _c_void_p, _i64, _c_void_p, _c_void_p, _i32,
+                                       _c_void_p, _c_void_p]),
+    "pntf_tt_act_fwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _c_void_p, _i64,
+                                       ctypes.c_int, ctypes.c_int, _c_void_p]),
+    "pntf_tt_act_bwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _i64, ctypes.c_int,
+                                       ctypes.c_int, _c_void_p, ctypes.c_int, _c_void_p,
+                                       _c_void_p]),
+    "pntf_tt_merge_fwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "pntf_tt_merge_bwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                         _c_void_p]),
+    "pntf_tt_head_loss": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _c_void_p,
+                                         _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32,
+                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                         _c_void_p]),
+    "pntf_adamw": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32,
+                                  _f32, _f32, _f32, _i64, _c_void_p]),
 }
 
 _lib = None
@@ -84,5 +103,7 @@ def load():
 def check(status, what):
     if status != 0:
         lib = load()
+        err = (lib.pntf_tt_last_error() if what.startswith(("pntf_tt_", "pntf_adamw"))
+               else lib.pntf_last_error()).decode()
         raise PntfError("%s failed: %s (%s)" % (
-            what, lib.pntf_status_string(status).decode(), lib.pntf_last_error().decode()))
+            what, lib.pntf_status_string(status).decode(), err))

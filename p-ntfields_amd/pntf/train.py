@@ -1,0 +1,249 @@
+"""Training step on MI355X: the weight gradient of the Eikonal residual loss and AdamW.
+
+Reference: one inner step of `Model.train` is
+    loss, loss_n, diff = self.Loss(points, speed, B, beta, gamma)   # :1040-1046
+    loss.backward(); optimizer.step(); optimizer.zero_grad()        # :1048-1052
+with `torch.optim.AdamW(lr=1e-3, weight_decay=0.1)` (:959-961) — models/model_res_sigmoid_multi.py
+(arm: models/model_res_sigmoid.py:954-956, 1062-1075).  The reference differentiates its
+Taylor-mode graph `NN.out_laplace` (:710-848) with autograd; here the adjoint is explicit:
+
+  forward  Φ planes (tt_fourier) → per Linear: one fp32 GEMM over all R·M Taylor rows
+           (torch.mm → hipBLASLt) + a fused bias/act_laplace kernel (tt_act_fwd) that keeps the
+           pre-activation as the tape → merge (tt_merge_fwd) → generator → generator[3]
+  head     generator[4] + actout_laplace + Model.Loss forward and backward in one kernel
+           (tt_head_loss): diff per pair and d(Σdiff)/d(generator[3] output)
+  backward per Linear, reversed: fused act_laplace adjoint + bias gradient (tt_act_bwd), the
+           weight gradient gW = gYᵀ·X as ONE GEMM over all R·M rows, the input gradient gY·W
+           (+ the residual branch through addmm's accumulate) → merge adjoint (tt_merge_bwd)
+
+Layout: a Taylor tensor of M points and width W is (R, M, W) fp32, R = 1 + 2·ndir planes
+[value | ∂ (ndir) | diagonal ∂² (ndir)], ndir = dim in the encoder and 2·dim after the merge.
+The GEMMs are plain library GEMMs (fp32, TF32 off); every elementwise stage is a HIP kernel
+of libpntf.so (csrc/pntf_train.hip).  There is no CPU path.
+"""
+import ctypes
+
+import torch
+
+from . import _lib, ops
+from ._lib import PntfError, check
+
+H = 128
+_BLOCK_HEADS = ("encoder.1", "encoder.2", "generator.0", "generator.1", "generator.2")
+
+
+def trained_keys():
+    """State-dict keys that receive gradients (encoder1.0 is created at :160 but never used,
+    so the reference's AdamW skips it)."""
+    from .synth import state_dict_keys
+    return [k for k in state_dict_keys() if not k.startswith("encoder1.0.")]
+
+
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(None)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_partial_cache = {}
+
+
+def _partial(device):
+    key = (device.type, device.index)
+    buf = _partial_cache.get(key)
+    if buf is None:
+        buf = torch.empty(int(_lib.load().pntf_tt_partial_floats()), dtype=torch.float32,
+                          device=device)
+        _partial_cache[key] = buf
+    return buf
+
+
+class _Tape:
+    """Forward tape of one loss evaluation: (name, input planes, pre-activation planes, act,
+    has_residual) per Linear, in execution order."""
+
+    def __init__(self, params, dim, device):
+        self.p = params
+        self.dim = dim
+        self.dev = device
+        self.s = _stream(device)
+        self.lib = _lib.load()
+        self.ops = []
+
+    def lin(self, x3, name, act=True, res=None):
+        W, b = self.p[name + ".weight"], self.p[name + ".bias"]
+        R, M, K = x3.shape
+        N = W.shape[0]
+        y = torch.empty((R, M, N), dtype=torch.float32, device=self.dev)
+        if res is None:
+            torch.mm(x3.view(R * M, K), W.t(), out=y.view(R * M, N))
+        else:
+            torch.addmm(res.view(R * M, N), x3.view(R * M, K), W.t(), out=y.view(R * M, N))
+        h = torch.empty_like(y) if act else None
+        check(self.lib.pntf_tt_act_fwd((R - 1) // 2, _vp(y), _vp(h), _vp(b), M, N, int(act),
+                                       self.s), "pntf_tt_act_fwd")
+        self.ops.append((name, x3, y, act, res is not None))
+        return h if act else y
+
+
+def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
+    """diff (n,) of Model.Loss and, into `grads` (key -> tensor shaped like the parameter),
+    the gradient of scale·Σ diff w.r.t. every trained parameter.
+
+    params: state-dict key -> fp32 contiguous device tensor; xp (n, 2dim); yobs (n, 2);
+    Btab (n_env, dim, 128); env (n,) int32 or None."""
+    dev = xp.device
+    lib = _lib.load()
+    n = xp.shape[0]
+    if n == 0:
+        for g in grads.values():
+            g.zero_()
+        return torch.empty(0, dtype=torch.float32, device=dev)
+    if torch.backends.cuda.matmul.allow_tf32:
+        raise PntfError("TF32 GEMMs are enabled; the training step computes in fp32")
+    tape = _Tape(params, dim, dev)
+    s = tape.s
+    Re, Rg = 1 + 2 * dim, 1 + 4 * dim
+    phi = torch.empty((Re, 2 * n, 2 * H), dtype=torch.float32, device=dev)
+    n_env = Btab.shape[0]
+    check(lib.pntf_tt_fourier(dim, _vp(xp), n, _vp(Btab), _vp(env), n_env, _vp(phi), s),
+          "pntf_tt_fourier")
+    h = tape.lin(phi, "encoder.0")
+    for i in (1, 2):
+        a = tape.lin(h, "encoder.%d" % i)
+        h = tape.lin(a, "encoder1.%d" % i, res=h)
+    z = tape.lin(h, "encoder.3", act=False)
+    u = torch.empty((Rg, n, 2 * H), dtype=torch.float32, device=dev)
+    check(lib.pntf_tt_merge_fwd(dim, _vp(z), n, _vp(u), s), "pntf_tt_merge_fwd")
+    for i in (0, 1, 2):
+        a = tape.lin(u, "generator.%d" % i)
+        u = tape.lin(a, "generator1.%d" % i, res=u)
+    v = tape.lin(u, "generator.3")
+    diff = torch.empty(n, dtype=torch.float32, device=dev)
+    g = torch.empty_like(v)
+    part = _partial(dev)
+    check(lib.pntf_tt_head_loss(dim, int(arm), _vp(v), _vp(params["generator.4.weight"]),
+                                _vp(params["generator.4.bias"]), _vp(xp), _vp(yobs), n,
+                                float(gamma), float(scale), _vp(diff), _vp(g),
+                                _vp(grads["generator.4.weight"]), _vp(grads["generator.4.bias"]),
+                                _vp(part), s), "pntf_tt_head_loss")
+    pending = []
+    for name, x3, y, act, has_res in reversed(tape.ops):
+        R, M, K = x3.shape
+        N = y.shape[2]
+        check(lib.pntf_tt_act_bwd((R - 1) // 2, _vp(y), _vp(g), M, N, int(act),
+                                  _vp(grads[name + ".bias"]), 0, _vp(part), s),
+              "pntf_tt_act_bwd")
+        g2 = g.view(R * M, N)
+        torch.mm(g2.t(), x3.view(R * M, K), out=grads[name + ".weight"])
+        if name == "encoder.0":
+            break
+        if has_res:
+            pending.append(g)
+        gx = torch.empty((R, M, K), dtype=torch.float32, device=dev)
+        W = params[name + ".weight"]
+        if name in _BLOCK_HEADS:      # the block input also fed the residual add
+            torch.addmm(pending.pop().view(R * M, K), g2, W, out=gx.view(R * M, K))
+        else:
+            torch.mm(g2, W, out=gx.view(R * M, K))
+        g = gx
+        if name == "generator.0":
+            gz = torch.empty((Re, 2 * n, H), dtype=torch.float32, device=dev)
+            check(lib.pntf_tt_merge_bwd(dim, _vp(z), _vp(g), n, _vp(gz), s), "pntf_tt_merge_bwd")
+            g = gz
+    return diff
+
+
+def module_params(module):
+    """The trained parameters of an NN module as {key: fp32 contiguous device tensor}."""
+    sd = module.state_dict(keep_vars=True)
+    out = {}
+    for k in trained_keys():
+        p = sd[k]
+        ops._require_device(p, k)
+        if p.dtype != torch.float32 or not p.is_contiguous():
+            raise PntfError("parameter %s must be fp32 contiguous" % k)
+        out[k] = p.detach()
+    return out
+
+
+class EikonalLossFunction(torch.autograd.Function):
+    """Σdiff·scale of Model.Loss with a HIP backward to the weights.  The adjoint sweep runs
+    inside forward (its head kernel fuses the loss backward), the weight gradients wait in
+    ctx until autograd asks for them.  Inputs (points, speeds, B) get no gradient: the
+    reference never reads theirs."""
+
+    @staticmethod
+    def forward(ctx, xp, yobs, Btab, env, dim, gamma, scale, arm, keys, *params):
+        p = {k: t.detach() for k, t in zip(keys, params)}
+        grads = {k: torch.empty_like(t) for k, t in p.items()}
+        diff = loss_grad(p, xp, yobs, Btab, env, dim, gamma, scale, arm, grads)
+        ctx.grads = [grads[k] for k in keys]
+        ctx.mark_non_differentiable(diff)
+        total = ops.device_sum(diff).float() * scale
+        return total, diff
+
+    @staticmethod
+    def backward(ctx, g_total, g_diff):
+        gs = ctx.grads
+        ctx.grads = None
+        return (None,) * 9 + tuple(g * g_total for g in gs)
+
+
+def eikonal_loss(module, xp, yobs, Btab, env, dim, gamma, scale, arm=False):
+    """(scale·Σdiff (0-d, differentiable w.r.t. the module's parameters), diff (n,))."""
+    ops._require_device(xp, "points")
+    xp = xp.detach().to(torch.float32).contiguous()
+    yobs = yobs.detach().to(device=xp.device, dtype=torch.float32).contiguous()
+    Btab = Btab.detach().to(device=xp.device, dtype=torch.float32).contiguous()
+    if env is not None:
+        env = env.to(device=xp.device, dtype=torch.int32).contiguous()
+    if xp.dim() != 2 or xp.shape[1] != 2 * dim or yobs.shape != (xp.shape[0], 2):
+        raise PntfError("points must be (n, %d) and speeds (n, 2)" % (2 * dim))
+    if Btab.dim() != 3 or Btab.shape[1:] != (dim, H):
+        raise PntfError("B table must be (n_env, %d, 128)" % dim)
+    p = module_params(module)
+    keys = list(p.keys())
+    sd = module.state_dict(keep_vars=True)
+    return EikonalLossFunction.apply(xp, yobs, Btab, env, dim, float(gamma), float(scale),
+                                     bool(arm), keys, *[sd[k] for k in keys])
+
+
+class AdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW semantics (the reference's optimizer, :959-961) with the update as one
+    fused HIP kernel per parameter (pntf_adamw).  Parameters without a gradient are skipped,
+    exactly as torch does (encoder1.0).  state_dict()/load_state_dict() work as in torch, so
+    the reference's rollback of (network, optimizer) states (:1093-1101) is unchanged."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = _lib.load()
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                ops._require_device(p, "param")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                g = p.grad.contiguous()
+                check(lib.pntf_adamw(_vp(p), _vp(g), _vp(st["exp_avg"]), _vp(st["exp_avg_sq"]),
+                                     p.numel(), float(group["lr"]), float(b1), float(b2),
+                                     float(group["eps"]), float(group["weight_decay"]),
+                                     int(st["step"].item()), _stream(p.device)), "pntf_adamw")
+                # the kernel wrote through a raw pointer: tell torch (and PackedCache)
+                torch.autograd.graph.increment_version(p)
+        return loss

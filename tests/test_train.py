@@ -1,0 +1,207 @@
+"""Training step: weight gradients of Model.Loss and the AdamW update.
+
+Pinning: tests/golden/train_d{3,6}.npz hold the reference's own `loss.backward()` gradients
+and its torch.optim.AdamW parameters after two steps (tests/golden/make_train_goldens.py,
+imports the reference).  The CPU tests pin the oracle's hand-derived adjoint
+(oracle.eikonal_loss_grad) to them; the GPU tests compare the HIP Taylor-tape path with
+both.  Tolerance: each parameter's gradient within 2e-4 of the golden relative to that
+parameter's max |gradient| (fp32 GEMM sums over up to 13·n Taylor rows).  AdamW itself is
+checked against torch.optim.AdamW on identical gradients (a few fp32 ulp).  End to end, two
+steps from the reference's state: Adam normalises every coordinate (|update| ≈ lr whatever
+the gradient's size), so a near-zero gradient whose fp32 rounding differs can move a weight
+by up to 2·lr per step; 99 % of the weights must agree within 1e-6 and all within 4·lr.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import load, weights
+from oracle import pntf_oracle as O
+from pntf import synth
+
+GRAD_TOL = 2e-4
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _golden_case(name):
+    f = load(name)
+    if name == "train_d3.npz":
+        E, n = f["pts"].shape[:2]
+        xp = f["pts"].reshape(E * n, -1)
+        yobs = f["yobs"].reshape(E * n, 2)
+        return f, dict(xp=xp, yobs=yobs, B=f["B_table"], env=np.repeat(np.arange(E), n)
+                       .astype(np.int32), dim=3, scale=float(f["beta"]) / (E * n), arm=False)
+    xp = f["pts"]
+    return f, dict(xp=xp, yobs=f["yobs"], B=f["B"].T[None], env=None, dim=6,
+                   scale=float(f["beta"]) / xp.shape[0], arm=True)
+
+
+# ---------------------------------------------------------------- CPU: oracle pinned
+
+
+@pytest.mark.parametrize("name", ["train_d3.npz", "train_d6.npz"])
+def test_oracle_weight_grads_vs_reference(name):
+    W = weights()
+    f, c = _golden_case(name)
+    B = c["B"][0] if c["env"] is None else c["B"]
+    diff, g = O.eikonal_loss_grad(W, c["xp"], c["yobs"], B, c["env"], c["dim"],
+                                  float(f["gamma"]), c["scale"], c["arm"])
+    assert np.abs(diff - f["diff"].reshape(-1)).max() < 1e-5
+    keys = [k for k in f.files if k.startswith("grad:")]
+    assert len(keys) == 28 and "grad:encoder1.0.weight" not in keys
+    assert set(g) == {k[5:] for k in keys}
+    for k in keys:
+        assert _rel(g[k[5:]], f[k]) < 5e-5, k
+
+
+def test_oracle_adamw_matches_torch():
+    rng = np.random.default_rng(3)
+    p0 = rng.standard_normal(257)
+    grads = [rng.standard_normal(257) * 1e-2 for _ in range(3)]
+    tp = torch.nn.Parameter(torch.tensor(p0))
+    opt = torch.optim.AdamW([tp], lr=1e-3, weight_decay=0.1)
+    p, m, v = p0.copy(), np.zeros_like(p0), np.zeros_like(p0)
+    for s, g in enumerate(grads, 1):
+        tp.grad = torch.tensor(g)
+        opt.step()
+        O.adamw_step(p, g, m, v, s)
+    assert np.abs(p - tp.detach().numpy()).max() < 1e-12
+
+
+# ---------------------------------------------------------------- GPU: HIP Taylor tape
+
+
+def _nets(dim, W, dev, B=None):
+    if dim == 3:
+        from models import model_res_sigmoid_multi as md
+        net = md.NN(dev, 3)
+        model = md.Model(".", ".", 3, 2, device=dev)
+    else:
+        from models import model_res_sigmoid as ma
+        net = ma.NN(dev, 6, torch.from_numpy(B))
+        model = ma.Model(".", ".", 6, device=dev)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    net.to(dev).float()
+    model.network = net
+    return model, net
+
+
+def _loss(model, f, dim, dev):
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    pts = T(f["pts"]).requires_grad_()
+    if dim == 3:
+        return model.Loss(pts, T(f["yobs"]), T(f["B_table"]), float(f["beta"]), float(f["gamma"]))
+    return model.Loss(pts, T(f["yobs"]), float(f["beta"]), float(f["gamma"]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,dim", [("train_d3.npz", 3), ("train_d6.npz", 6)])
+def test_loss_backward_vs_reference(name, dim):
+    dev = torch.device("cuda:0")
+    W = weights()
+    f = load(name)
+    model, net = _nets(dim, W, dev, f["B"] if dim == 6 else None)
+    loss, loss_n, diff = _loss(model, f, dim, dev)
+    assert abs(loss_n.item() - float(f["loss_n"])) < 1e-5 * max(1.0, abs(float(f["loss_n"])))
+    assert np.abs(diff.detach().cpu().numpy() - f["diff"]).max() < 1e-4
+    loss.backward()
+    for k, p in net.named_parameters():
+        if "grad:" + k in f.files:
+            assert p.grad is not None, k
+            assert _rel(p.grad.cpu().numpy(), f["grad:" + k]) < GRAD_TOL, k
+        else:
+            assert p.grad is None, k            # encoder1.0: never used, no gradient
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,dim", [("train_d3.npz", 3), ("train_d6.npz", 6)])
+def test_two_adamw_steps_vs_reference(name, dim):
+    from pntf.train import AdamW
+    dev = torch.device("cuda:0")
+    W = weights()
+    f = load(name)
+    model, net = _nets(dim, W, dev, f["B"] if dim == 6 else None)
+    opt = AdamW(net.parameters(), lr=1e-3, weight_decay=0.1)
+    for step in range(2):
+        loss, loss_n, _ = _loss(model, f, dim, dev)
+        if step == 1:
+            assert abs(loss.item() - float(f["loss2"])) < 1e-5 * max(1.0, float(f["loss2"]))
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+    sd = net.state_dict()
+    for k in f.files:
+        if k.startswith("after2:"):
+            err = np.abs(sd[k[7:]].cpu().numpy() - f[k])
+            assert np.mean(err < 1e-6) >= 0.99 and err.max() < 4e-3, (k, err.max())
+    assert np.array_equal(sd["encoder1.0.weight"].cpu().numpy(), W["encoder1.0.weight"])
+
+
+@pytest.mark.gpu
+def test_adamw_kernel_vs_torch():
+    from pntf.train import AdamW
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(5)
+    shapes = [(128, 256), (256,), (1, 128), (1,)]
+    p0 = [torch.randn(s, generator=g) for s in shapes]
+    grads = [[torch.randn(s, generator=g) * 1e-2 for s in shapes] for _ in range(3)]
+    ours = [torch.nn.Parameter(p.clone().to(dev)) for p in p0]
+    ref = [torch.nn.Parameter(p.clone().to(dev)) for p in p0]
+    o1 = AdamW(ours, lr=1e-3, weight_decay=0.1)
+    o2 = torch.optim.AdamW(ref, lr=1e-3, weight_decay=0.1, foreach=False)
+    for gs in grads:
+        for a, b, gg in zip(ours, ref, gs):
+            a.grad = gg.to(dev)
+            b.grad = gg.to(dev)
+        o1.step()
+        o2.step()
+    for a, b in zip(ours, ref):
+        # fp32 operation-order rounding only: a few ulp
+        assert torch.allclose(a.detach(), b.detach(), rtol=5e-7, atol=1e-8)
+    st = o1.state_dict()
+    assert st["state"][0]["step"].item() == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 37, 300])
+def test_weight_grads_ragged_multi_env_vs_oracle(n):
+    """Per-pair env ids in random order (not contiguous), ragged sizes; fp64 oracle."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    W = weights()
+    xp = synth.make_pairs(n, 3, seed=40 + n)
+    yobs = synth.make_speeds(n, seed=41 + n)
+    Bt = synth.make_B_table(3, 3, first_seed=31)
+    env = synth.make_env_ids(n, 3, contiguous=False, seed=n)
+    diff_o, g_o = O.eikonal_loss_grad(W, xp, yobs, Bt, env, 3, 1e-3, 1.0 / n)
+    params = {k: torch.from_numpy(W[k]).to(dev) for k in train.trained_keys()}
+    grads = {k: torch.empty_like(v) for k, v in params.items()}
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    diff = train.loss_grad(params, T(xp), T(yobs), T(Bt), T(env), 3, 1e-3, 1.0 / n, False,
+                           grads)
+    assert _rel(diff.cpu().numpy(), diff_o) < 1e-4
+    for k in params:
+        assert _rel(grads[k].cpu().numpy(), g_o[k]) < GRAD_TOL, k
+
+
+@pytest.mark.gpu
+def test_training_loss_matches_inference_loss():
+    """Model.Loss under no_grad (fused residual kernel) and with grad (Taylor tape) agree."""
+    from models import model_res_sigmoid_multi as md
+    dev = torch.device("cuda:0")
+    W = weights()
+    f = load("loss_d3.npz")
+    model, net = _nets(3, W, dev)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    with torch.no_grad():
+        _, ln0, d0 = model.Loss(T(f["pts"]), T(f["yobs"]), T(f["B_table"]), 1.0, 1e-3)
+    _, ln1, d1 = model.Loss(T(f["pts"]), T(f["yobs"]), T(f["B_table"]), 1.0, 1e-3)
+    assert ln1.requires_grad and not ln0.requires_grad
+    assert abs(ln0.item() - ln1.item()) < 1e-5 * max(1.0, abs(ln0.item()))
+    assert _rel(d1.detach().cpu().numpy(), d0.cpu().numpy()) < 1e-4
+    assert md is not None

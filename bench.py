@@ -235,8 +235,54 @@ def extras(packed, dev):
                                  mode=ops.GRAD_BACKGRAD_COMPAT, schedule=sched)
         ms = timeit(run1, reps=2)
         out["gib_plan_q1_ms_per_step_" + sched] = ms / 100.0
+    out.update(train_extras(dev))
+    return out
+
+
+TRAIN_FLOP_PER_PAIR = 3 * 14_286_848   # Taylor forward + 2x for the adjoint (GEMM MACs x 2)
+
+
+def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=5):
+    """Model.train inner step (model_res_sigmoid_multi.py:1040-1052) on the HIP Taylor tape:
+    Loss forward + loss.backward() + AdamW step.  (2, 10000) is the reference's batch
+    (Batch Size 2 environments x inner_batch 10000 pairs, :1010-1036)."""
+    from models import model_res_sigmoid_multi as md
+    from pntf.train import AdamW
+    out = {}
+    W = synth.make_weights(0)
+    net = md.NN(dev, 3)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    net.to(dev)
+    model = md.Model(".", ".", 3, 2, device=dev)
+    model.network = net
+    opt = AdamW(net.parameters(), lr=1e-3, weight_decay=0.1)
+    for E, n in sizes:
+        pts = torch.from_numpy(synth.make_pairs(E * n, 3, seed=77).reshape(E, n, 6)).to(dev)
+        yobs = torch.from_numpy(synth.make_speeds(E * n, seed=78).reshape(E, n, 2)).to(dev)
+        Bt = torch.from_numpy(synth.make_B_table(E, 3, first_seed=21)).to(dev)
+
+        def step():
+            loss, _, _ = model.Loss(pts, yobs, Bt, 1.0, 1e-3)
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+        step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        tag = "train_step_%dx%d" % (E, n)
+        out[tag + "_ms"] = ms
+        out[tag + "_pairs_per_s"] = E * n / (ms * 1e-3)
+        out[tag + "_TFLOPs"] = TRAIN_FLOP_PER_PAIR * E * n / (ms * 1e-3) / 1e12
     return out
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--train-only":
+        torch.cuda.set_device(0)
+        print(json.dumps(train_extras(torch.device("cuda", 0))), flush=True)
+        sys.exit(0)
     main()

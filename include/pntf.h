@@ -154,11 +154,12 @@ const char* pntf_tt_last_error(void);
 int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, const int32_t* env,
                     int32_t n_env, float* phi, hipStream_t stream);
 
-/* Bias + act_laplace (:663-691) on GEMM output y (R, m, w), w = 128|256, ndir = 3|6|12:
- * y's value plane += bias (y is kept as the tape); act != 0: h (R, m, w) = softplus10 Taylor
- * rows.  act == 0 (Linear without activation): bias only, h unused. */
-int pntf_tt_act_fwd(int ndir, float* y, float* h, const float* bias, int64_t m, int w, int act,
-                    hipStream_t stream);
+/* Bias (+ residual) + act_laplace (:663-691, residual :744/:828) on GEMM output y (R, m, w),
+ * w = 128|256, ndir = 3|6|12: y's value plane += bias, every plane += res (R, m, w) when res
+ * is not NULL (y is kept as the tape); act != 0: h (R, m, w) = softplus10 Taylor rows.
+ * act == 0 (Linear without activation, res must be NULL): bias only, h unused. */
+int pntf_tt_act_fwd(int ndir, float* y, float* h, const float* bias, const float* res,
+                    int64_t m, int w, int act, hipStream_t stream);
 
 /* Adjoint of pntf_tt_act_fwd, in place: g (R, m, w) holds dL/dh on entry and dL/dy on exit
  * (act == 0: unchanged); gbias (w) (+)= sum over points of dL/dy's value plane

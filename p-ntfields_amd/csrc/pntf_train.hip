@@ -105,20 +105,29 @@ __global__ void tt_fourier_kernel(const float* __restrict__ xp, int64_t n,
 // ---------------------------------------------------------------- act_laplace (:675-691)
 // y (R, M, W): GEMM output; plane 0 gets the bias (kept in place as the saved
 // pre-activation).  ACT: h = softplus10(y), J' = σJ, L' = σ'J² + σL (σ = σ(10y), σ' = 10σ(1-σ)).
-template <int NDIR, bool ACT>
+// RES: the residual branch (:744, :828) res (R, M, W) is added to every plane first (and
+// the sum kept in y).
+template <int NDIR, bool ACT, bool RES>
 __global__ void tt_act_fwd_kernel(float* __restrict__ y, float* __restrict__ h,
-                                  const float* __restrict__ bias, int64_t M, int W) {
+                                  const float* __restrict__ bias, const float* __restrict__ res,
+                                  int64_t M, int W) {
   const int64_t plane = M * W;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < plane;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const float v = y[i] + bias[i % W];
+    const float v = y[i] + bias[i % W] + (RES ? res[i] : 0.f);
     y[i] = v;
     if (!ACT) continue;
     const float s = sig10(v), ds = SCALE * s * (1.f - s);
     h[i] = softplus10(v);
 #pragma unroll
     for (int k = 0; k < NDIR; ++k) {
-      const float J = y[(1 + k) * plane + i], L = y[(1 + NDIR + k) * plane + i];
+      float J = y[(1 + k) * plane + i], L = y[(1 + NDIR + k) * plane + i];
+      if (RES) {
+        J += res[(1 + k) * plane + i];
+        L += res[(1 + NDIR + k) * plane + i];
+        y[(1 + k) * plane + i] = J;
+        y[(1 + NDIR + k) * plane + i] = L;
+      }
       h[(1 + k) * plane + i] = J * s;
       h[(1 + NDIR + k) * plane + i] = fmaf(J * J, ds, L * s);
     }
@@ -424,16 +433,20 @@ int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, cons
   return check_launch("tt_fourier_kernel");
 }
 
-int pntf_tt_act_fwd(int ndir, float* y, float* h, const float* bias, int64_t m, int w, int act,
-                    hipStream_t stream) {
+int pntf_tt_act_fwd(int ndir, float* y, float* h, const float* bias, const float* res,
+                    int64_t m, int w, int act, hipStream_t stream) {
   if ((ndir != 3 && ndir != 6 && ndir != 12) || m < 0 || (w != 128 && w != 256) ||
-      (m > 0 && (!y || !bias || (act && !h))))
+      (m > 0 && (!y || !bias || (act && !h))) || (res && !act))
     return fail("pntf_tt_act_fwd: bad arguments");
   if (m == 0) return PNTF_OK;
   const dim3 g(grid_1d(m * w)), b(256);
 #define PNTF_ACT_FWD(N)                                                                   \
-  if (act) hipLaunchKernelGGL((tt_act_fwd_kernel<N, true>), g, b, 0, stream, y, h, bias, m, w); \
-  else hipLaunchKernelGGL((tt_act_fwd_kernel<N, false>), g, b, 0, stream, y, h, bias, m, w);
+  if (res) hipLaunchKernelGGL((tt_act_fwd_kernel<N, true, true>), g, b, 0, stream, y, h, bias, \
+                              res, m, w);                                                 \
+  else if (act) hipLaunchKernelGGL((tt_act_fwd_kernel<N, true, false>), g, b, 0, stream, y, h, \
+                                   bias, res, m, w);                                      \
+  else hipLaunchKernelGGL((tt_act_fwd_kernel<N, false, false>), g, b, 0, stream, y, h, bias, \
+                          res, m, w);
   if (ndir == 3) { PNTF_ACT_FWD(3) }
   else if (ndir == 6) { PNTF_ACT_FWD(6) }
   else { PNTF_ACT_FWD(12) }

@@ -57,8 +57,8 @@ SIGNATURES = {
     "pntf_tt_last_error": (ctypes.c_char_p, []),
     "pntf_tt_fourier": (ctypes.c_int, [ctypes.c_int, _c_void_p, _i64, _c_void_p, _c_void_p, _i32,
                                        _c_void_p, _c_void_p]),
-    "pntf_tt_act_fwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _c_void_p, _i64,
-                                       ctypes.c_int, ctypes.c_int, _c_void_p]),
+    "pntf_tt_act_fwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                       _i64, ctypes.c_int, ctypes.c_int, _c_void_p]),
     "pntf_tt_act_bwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _i64, ctypes.c_int,
                                        ctypes.c_int, _c_void_p, ctypes.c_int, _c_void_p,
                                        _c_void_p]),

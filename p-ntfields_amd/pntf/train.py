@@ -8,13 +8,14 @@ with `torch.optim.AdamW(lr=1e-3, weight_decay=0.1)` (:959-961) — models/model_
 Taylor-mode graph `NN.out_laplace` (:710-848) with autograd; here the adjoint is explicit:
 
   forward  Φ planes (tt_fourier) → per Linear: one fp32 GEMM over all R·M Taylor rows
-           (torch.mm → hipBLASLt) + a fused bias/act_laplace kernel (tt_act_fwd) that keeps the
-           pre-activation as the tape → merge (tt_merge_fwd) → generator → generator[3]
+           (torch.mm → hipBLASLt) + a fused bias/residual/act_laplace kernel (tt_act_fwd) that
+           keeps the pre-activation as the tape → merge (tt_merge_fwd) → generator → generator[3]
   head     generator[4] + actout_laplace + Model.Loss forward and backward in one kernel
            (tt_head_loss): diff per pair and d(Σdiff)/d(generator[3] output)
   backward per Linear, reversed: fused act_laplace adjoint + bias gradient (tt_act_bwd), the
            weight gradient gW = gYᵀ·X as ONE GEMM over all R·M rows, the input gradient gY·W
-           (+ the residual branch through addmm's accumulate) → merge adjoint (tt_merge_bwd)
+           (+ the residual branch, accumulated in place by the GEMM) → merge adjoint
+           (tt_merge_bwd)
 
 Layout: a Taylor tensor of M points and width W is (R, M, W) fp32, R = 1 + 2·ndir planes
 [value | ∂ (ndir) | diagonal ∂² (ndir)], ndir = dim in the encoder and 2·dim after the merge.
@@ -77,15 +78,35 @@ class _Tape:
         R, M, K = x3.shape
         N = W.shape[0]
         y = torch.empty((R, M, N), dtype=torch.float32, device=self.dev)
-        if res is None:
-            torch.mm(x3.view(R * M, K), W.t(), out=y.view(R * M, N))
-        else:
-            torch.addmm(res.view(R * M, N), x3.view(R * M, K), W.t(), out=y.view(R * M, N))
+        torch.mm(x3.view(R * M, K), W.t(), out=y.view(R * M, N))
         h = torch.empty_like(y) if act else None
-        check(self.lib.pntf_tt_act_fwd((R - 1) // 2, _vp(y), _vp(h), _vp(b), M, N, int(act),
-                                       self.s), "pntf_tt_act_fwd")
+        check(self.lib.pntf_tt_act_fwd((R - 1) // 2, _vp(y), _vp(h), _vp(b), _vp(res), M, N,
+                                       int(act), self.s), "pntf_tt_act_fwd")
         self.ops.append((name, x3, y, act, res is not None))
         return h if act else y
+
+
+_SPLIT_ROWS = 8192      # rows per split-K chunk of a weight-gradient GEMM
+_SPLIT_MAX = 64
+
+
+def weight_grad(g2, x2, out):
+    """out (N, K) = g2ᵀ (N, rows) · x2 (rows, K).  The reduction runs over every Taylor row of
+    every point (rows = R·M, 10⁵-10⁶) into a tiny 128/256-square output: as one GEMM it has
+    only a handful of output tiles for 256 CUs (measured 15-42 TFLOP/s).  Split-K instead: S
+    row chunks as one batched GEMM (S·tiles workgroups), then a sum over the S partials."""
+    rows, N = g2.shape
+    K = x2.shape[1]
+    S = min(_SPLIT_MAX, rows // _SPLIT_ROWS)
+    if S < 2:
+        torch.mm(g2.t(), x2, out=out)
+        return
+    c = rows // S
+    main = c * S
+    part = torch.bmm(g2[:main].view(S, c, N).transpose(1, 2), x2[:main].view(S, c, K))
+    torch.sum(part, dim=0, out=out)
+    if main < rows:
+        torch.addmm(out, g2[main:].t(), x2[main:], out=out)
 
 
 def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
@@ -137,16 +158,19 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
                                   _vp(grads[name + ".bias"]), 0, _vp(part), s),
               "pntf_tt_act_bwd")
         g2 = g.view(R * M, N)
-        torch.mm(g2.t(), x3.view(R * M, K), out=grads[name + ".weight"])
+        weight_grad(g2, x3.view(R * M, K), grads[name + ".weight"])
         if name == "encoder.0":
             break
         if has_res:
             pending.append(g)
-        gx = torch.empty((R, M, K), dtype=torch.float32, device=dev)
         W = params[name + ".weight"]
-        if name in _BLOCK_HEADS:      # the block input also fed the residual add
-            torch.addmm(pending.pop().view(R * M, K), g2, W, out=gx.view(R * M, K))
+        if name in _BLOCK_HEADS:
+            # the block input also fed the residual add: accumulate into that branch's
+            # gradient in place (beta = 1, no copy); it is not read again
+            gx = pending.pop()
+            torch.addmm(gx.view(R * M, K), g2, W, out=gx.view(R * M, K))
         else:
+            gx = torch.empty((R, M, K), dtype=torch.float32, device=dev)
             torch.mm(g2, W, out=gx.view(R * M, K))
         g = gx
         if name == "generator.0":

@@ -17,8 +17,10 @@ return shapes and state-dict keys are the reference's:
       .out_laplace(coords, B) -> (tau, dtau, ltau, coords)  :710-848 Taylor mode (HIP)
     Model.Loss(points, Yobs, B, beta, gamma)  :897-951 Eikonal residual (HIP), values only
 
-Compute needs HIP device tensors; there is no CPU path (PntfError otherwise).  Training
-(`train`, `Loss`'s weight backward) and `plot` are outside this round's hot path and raise.
+    Model.train()                              :953-1141 HIP Taylor-tape backward + AdamW
+
+Compute needs HIP device tensors; there is no CPU path (PntfError otherwise).  `plot`
+(matplotlib figures) is outside the hot path and raises.
 """
 import numpy as np
 import torch
@@ -193,8 +195,104 @@ class Model:
         return beta * loss_n, loss_n, diff
 
     def train(self):
-        raise NotImplementedError("training (Model.train, :953-1141) is outside the HIP hot "
-                                  "path of this round")
+        """Model.train (:953-1141): AdamW(lr 1e-3, wd 0.1) over the environment dataset
+        (data_multi.Database, 2 environments per batch), the progressive speed blend α, the
+        per-epoch lr clip, up to 6 inner steps of `inner_batch` (10000) shuffled pairs per
+        environment batch, and the rollback to one of the last 5 (network, optimizer) states
+        when the epoch's mean residual grows by 1.2x or more.  Every inner step is
+        Loss → loss.backward() → optimizer.step() on the HIP Taylor tape (pntf/train.py).
+        Not reproduced: `plot` (matplotlib figures) at save time."""
+        import copy
+        import random
+        import time
+
+        from . import data_multi as db
+        P = self.Params
+        dev = torch.device(P["Device"])
+        self.network = NN(P["Device"], self.dim)
+        self.network.apply(self.network.init_weights)
+        self.network.to(dev)
+        self.optimizer = _train.AdamW(self.network.parameters(),
+                                      lr=P["Training"]["Learning Rate"], weight_decay=0.1)
+        if P["Training"]["Use Scheduler (bool)"]:
+            self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optimizer)
+        self.dataset = db.Database(P["DataPath"], dev, self.len)
+        dataloader = torch.utils.data.DataLoader(
+            self.dataset, batch_size=int(P["Training"]["Batch Size"]), num_workers=1,
+            shuffle=True)
+        beta, prev_diff, current_diff = 1.0, 1.0, 1.0
+        step = -2000.0 / 4000.0
+        current_state = copy.deepcopy(self.network.state_dict())
+        current_optimizer = copy.deepcopy(self.optimizer.state_dict())
+        prev_state_queue, prev_optimizer_queue = [], []
+        inner_batch = int(P["Training"].get("Inner Batch", 10000))
+        inner_rows = self.dataset[0][0].shape[0]
+        inner_size = max(1, int(inner_rows / inner_batch))
+        for epoch in range(1, P["Training"]["Number of Epochs"] + 1):
+            alpha = min(max(0.5, 0.5 + 0.5 * step), 1.07)
+            step += 1.0 / 4000 / (int(epoch / 4000) + 1.0)
+            gamma = 0.001
+            prev_state_queue.append(current_state)
+            prev_optimizer_queue.append(current_optimizer)
+            if len(prev_state_queue) > 5:
+                prev_state_queue.pop(0)
+                prev_optimizer_queue.pop(0)
+            current_state = copy.deepcopy(self.network.state_dict())
+            current_optimizer = copy.deepcopy(self.optimizer.state_dict())
+            self.optimizer.param_groups[0]["lr"] = float(
+                np.clip(1e-3 * (1 - (epoch - 8000) / 1000.0), a_min=5e-4, a_max=1e-3))
+            prev_diff = current_diff
+            t0 = time.time()
+            while True:
+                total_train_loss = 0
+                total_diff = 0
+                for data, B, _ in dataloader:
+                    data = data.to(dev)
+                    B = B.to(dev)
+                    points = data[:, :, :2 * self.dim]
+                    speed = alpha * data[:, :, 2 * self.dim:] + 1 - alpha
+                    idx0 = torch.randperm(inner_rows, device=dev)
+                    idx1 = torch.randperm(inner_rows, device=dev)
+                    E = points.shape[0]
+                    idx = [idx0, idx1] + [torch.randperm(inner_rows, device=dev)
+                                          for _ in range(E - 2)]
+                    points_sh = torch.stack([points[e, idx[e]] for e in range(E)])
+                    speed_sh = torch.stack([speed[e, idx[e]] for e in range(E)])
+                    for ii in range(inner_size):
+                        if ii > 5:
+                            break
+                        sl = slice(ii * inner_batch, (ii + 1) * inner_batch)
+                        bp, bs = points_sh[:, sl].contiguous(), speed_sh[:, sl].contiguous()
+                        self.B = B[0, :]
+                        loss_value, loss_n, _ = self.Loss(bp, bs, B, beta, gamma)
+                        loss_value.backward()
+                        self.optimizer.step()
+                        self.optimizer.zero_grad()
+                        total_train_loss += loss_value.detach()
+                        total_diff += loss_n.detach()
+                total_train_loss /= len(dataloader) * 5.0
+                total_diff /= len(dataloader) * 5.0
+                current_diff = total_diff
+                diff_ratio = current_diff / prev_diff
+                if 0 < diff_ratio < 1.2:
+                    break
+                with torch.no_grad():
+                    r = random.randint(0, len(prev_state_queue) - 1)
+                    self.network.load_state_dict(prev_state_queue[r], strict=True)
+                    self.optimizer.load_state_dict(prev_optimizer_queue[r])
+                print("RepeatEpoch = {} -- Loss = {:.4e} -- Alpha = {:.4e}".format(
+                    epoch, float(total_diff), alpha))
+            self.total_train_loss.append(total_train_loss)
+            beta = 1.0 / float(total_diff)
+            if P["Training"]["Use Scheduler (bool)"]:
+                self.scheduler.step(total_train_loss)
+            if epoch % P["Training"]["Print Every * Epoch"] == 0:
+                print("Epoch = {} -- Loss = {:.4e} -- Alpha = {:.4e} -- {:.3f} s".format(
+                    epoch, float(total_diff), alpha, time.time() - t0))
+            if (epoch % P["Training"]["Save Every * Epoch"] == 0 or
+                    epoch == P["Training"]["Number of Epochs"] or epoch == 1):
+                with torch.no_grad():
+                    self.save(epoch=epoch, val_loss=float(total_diff))
 
     def save(self, epoch="", val_loss=""):
         """Same checkpoint dict as the reference (:1143-1152)."""

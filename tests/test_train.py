@@ -205,3 +205,51 @@ def test_training_loss_matches_inference_loss():
     assert abs(ln0.item() - ln1.item()) < 1e-5 * max(1.0, abs(ln0.item()))
     assert _rel(d1.detach().cpu().numpy(), d0.cpu().numpy()) < 1e-4
     assert md is not None
+
+
+# ---------------------------------------------------------------- data format + Model.train
+
+
+def _write_envs(path, E=2, N=20000, dim=3):
+    from models import data_multi as db
+    for e in range(E):
+        db.write_environment(path, e, synth.make_pairs(N, dim, seed=60 + e),
+                             synth.make_speeds(N, seed=70 + e), synth.make_B(dim, seed=80 + e))
+
+
+def test_database_format_roundtrip(tmp_path):
+    """models/data_multi.py:17-32: points rounded through float16, [points | speed], B."""
+    from models import data_multi as db
+    base = str(tmp_path / "env")
+    _write_envs(base, E=2, N=64)
+    ds = db.Database(base, "cpu", 2)
+    data, B, idx = ds[1]
+    pts = synth.make_pairs(64, 3, seed=61)
+    assert data.shape == (64, 8) and data.dtype == torch.float32 and idx == 1
+    assert np.array_equal(data[:, :6].numpy(), pts.astype(np.float16).astype(np.float32))
+    assert np.array_equal(data[:, 6:].numpy(), synth.make_speeds(64, seed=71))
+    assert np.allclose(B.numpy(), synth.make_B(3, seed=81))
+    assert len(ds) == 2
+
+
+@pytest.mark.gpu
+def test_model_train_two_epochs(tmp_path):
+    """Model.train end to end on a synthetic 2-environment dataset in the reference's format:
+    finite decreasing-or-rolled-back loss, weights move, checkpoints reload."""
+    from models import model_res_sigmoid_multi as md
+    base = str(tmp_path / "env")
+    _write_envs(base, E=2, N=20000)
+    mp = tmp_path / "ckpt"
+    mp.mkdir()
+    torch.manual_seed(0)
+    model = md.Model(str(mp), base, 3, 2, device="cuda:0")
+    model.Params["Training"]["Number of Epochs"] = 2
+    model.train()
+    assert len(model.total_train_loss) == 2
+    assert all(np.isfinite(float(v)) for v in model.total_train_loss)
+    files = sorted(p.name for p in mp.iterdir())
+    assert len(files) == 2 and files[0].startswith("Model_Epoch_00001_")
+    m2 = md.Model(str(mp), base, 3, 2, device="cuda:0")
+    m2.load(str(mp / files[-1]))
+    for (k, a), b in zip(model.network.state_dict().items(), m2.network.state_dict().values()):
+        assert torch.equal(a, b), k

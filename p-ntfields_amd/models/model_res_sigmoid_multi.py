@@ -19,8 +19,9 @@ return shapes and state-dict keys are the reference's:
 
     Model.train()                              :953-1141 HIP Taylor-tape backward + AdamW
 
-Compute needs HIP device tensors; there is no CPU path (PntfError otherwise).  `plot`
-(matplotlib figures) is outside the hot path and raises.
+    Model.field_grid() / .plot(...)            :1250-1293 80x80 Speed/Tau/TravelTimes grid
+
+Compute needs HIP device tensors; there is no CPU path (PntfError otherwise).
 """
 import numpy as np
 import torch
@@ -201,7 +202,7 @@ class Model:
         environment batch, and the rollback to one of the last 5 (network, optimizer) states
         when the epoch's mean residual grows by 1.2x or more.  Every inner step is
         Loss → loss.backward() → optimizer.step() on the HIP Taylor tape (pntf/train.py).
-        Not reproduced: `plot` (matplotlib figures) at save time."""
+        At save time it writes the same plots (`plot`, HIP field grid) and checkpoint."""
         import copy
         import random
         import time
@@ -292,6 +293,8 @@ class Model:
             if (epoch % P["Training"]["Save Every * Epoch"] == 0 or
                     epoch == P["Training"]["Number of Epochs"] or epoch == 1):
                 with torch.no_grad():
+                    if P["Training"].get("Plot (bool)", True):
+                        self.plot(epoch, float(total_diff), alpha)
                     self.save(epoch=epoch, val_loss=float(total_diff))
 
     def save(self, epoch="", val_loss=""):
@@ -351,5 +354,38 @@ class Model:
         return ops.plan(self.network.packed(), XP, _as_table(B, XP.device), env, self.dim,
                         step, tol, max_iter, mode)
 
+    def field_grid(self, limit=0.5):
+        """The 80x80 evaluation grid of Model.plot (:1250-1275): start fixed at
+        (-0.25, -0.25, 0, ...), goal swept over [-limit, limit)^2 in the first two axes;
+        TravelTimes, Speed and Tau on the HIP kernels.  Returns numpy (X, Y, TT, V, TAU)."""
+        spacing = limit / 40.0
+        X, Y = np.meshgrid(np.arange(-limit, limit, spacing), np.arange(-limit, limit, spacing))
+        XP = np.zeros((X.size, 2 * self.dim), np.float32)
+        XP[:, 0] = -0.25
+        XP[:, 1] = -0.25
+        XP[:, self.dim + 0] = X.ravel()
+        XP[:, self.dim + 1] = Y.ravel()
+        XP = torch.from_numpy(XP).to(self._dev())
+        tt = self.TravelTimes(XP)
+        ss = self.Speed(XP)
+        tau = self.Tau(XP)
+        return (X, Y, tt.cpu().numpy().reshape(X.shape), ss.cpu().numpy().reshape(X.shape),
+                tau.cpu().numpy().reshape(X.shape))
+
     def plot(self, epoch, total_train_loss, alpha):
-        raise NotImplementedError("Model.plot (matplotlib field plots) is not on the hot path")
+        """Model.plot (:1250-1293): speed and τ maps with travel-time contours, saved as
+        <ModelPath>/plots<epoch>_<alpha>_<loss>_0.jpg and tauplots...; the field values come
+        from field_grid (HIP)."""
+        import matplotlib
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+        X, Y, TT, V, TAU = self.field_grid()
+        tag = str(epoch) + "_" + str(alpha) + "_" + str(round(total_train_loss, 4)) + "_0.jpg"
+        for prefix, field in (("/plots", V), ("/tauplots", TAU)):
+            fig = plt.figure()
+            ax = fig.add_subplot(111)
+            quad = ax.pcolormesh(X, Y, field, vmin=0, vmax=1)
+            ax.contour(X, Y, TT, np.arange(0, 3, 0.05), cmap="bone", linewidths=0.5)
+            plt.colorbar(quad, ax=ax, pad=0.1, label="Predicted Velocity")
+            plt.savefig(self.Params["ModelPath"] + prefix + tag, bbox_inches="tight")
+            plt.close(fig)

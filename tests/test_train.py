@@ -247,9 +247,31 @@ def test_model_train_two_epochs(tmp_path):
     model.train()
     assert len(model.total_train_loss) == 2
     assert all(np.isfinite(float(v)) for v in model.total_train_loss)
-    files = sorted(p.name for p in mp.iterdir())
+    files = sorted(p.name for p in mp.iterdir() if p.suffix == ".pt")
     assert len(files) == 2 and files[0].startswith("Model_Epoch_00001_")
+    assert len([p for p in mp.iterdir() if p.suffix == ".jpg"]) == 4      # plot() at saves
     m2 = md.Model(str(mp), base, 3, 2, device="cuda:0")
     m2.load(str(mp / files[-1]))
     for (k, a), b in zip(model.network.state_dict().items(), m2.network.state_dict().values()):
         assert torch.equal(a, b), k
+
+
+@pytest.mark.gpu
+def test_field_grid_vs_oracle():
+    """Model.plot's 80x80 grid (:1250-1275) against the fp64 oracle epilogues."""
+    from models import model_res_sigmoid_multi as md
+    dev = torch.device("cuda:0")
+    W = weights()
+    model, net = _nets(3, W, dev)
+    B = synth.make_B(3, seed=1)
+    model.B = torch.from_numpy(B)
+    X, Y, TT, V, TAU = model.field_grid()
+    assert X.shape == (80, 80)
+    xp = np.zeros((X.size, 6))
+    xp[:, :2] = -0.25
+    xp[:, 3], xp[:, 4] = X.ravel(), Y.ravel()
+    t, d = O.tau_grad(W, xp, B)
+    assert _rel(TAU.ravel(), t[:, 0]) < 1e-4
+    assert _rel(TT.ravel(), O.travel_time(xp, t)) < 1e-4
+    assert _rel(V.ravel(), O.speed(xp, t, d)) < 1e-3
+    assert md is not None

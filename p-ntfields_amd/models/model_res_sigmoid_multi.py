@@ -210,6 +210,7 @@ class Model:
         from . import data_multi as db
         P = self.Params
         dev = torch.device(P["Device"])
+        ops._require_device(torch.empty(0, device=dev), "Model.train device")   # no CPU path
         self.network = NN(P["Device"], self.dim)
         self.network.apply(self.network.init_weights)
         self.network.to(dev)

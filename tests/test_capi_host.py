@@ -104,8 +104,11 @@ def test_models_raise_on_cpu_compute():
     m.network = md.NN("cpu", 3)
     with pytest.raises(_lib.PntfError):
         m.network.out(torch.zeros(4, 6), torch.zeros(3, 128))
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(_lib.PntfError):
         m.train()
+    pts = torch.zeros(1, 4, 6, requires_grad=True)
+    with pytest.raises(_lib.PntfError):      # the training loss has no CPU path either
+        m.Loss(pts, torch.ones(1, 4, 2), torch.zeros(1, 3, 128), 1.0, 1e-3)
 
 
 def _pack_index_numpy(W, trans):

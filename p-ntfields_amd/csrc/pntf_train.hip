@@ -32,7 +32,7 @@ namespace {
 constexpr int H = 128;
 constexpr float SCALE = 10.f;               // Softplus beta (model_res_sigmoid_multi.py:140)
 constexpr float TWO_PI = 6.283185307179586f;
-constexpr int NB_MAX = 512;                 // partial-sum blocks of the reductions
+constexpr int NB_MAX = 512;                 // partial-sum blocks of the reductions (2/CU)
 
 thread_local char g_err[512] = "";
 
@@ -65,7 +65,7 @@ __device__ __forceinline__ float softplus10(float y) {
 // ---------------------------------------------------------------- Φ planes (:199-213)
 // phi (1 + 2 DIM, 2n, 256): point m < n is x_start of pair m, m >= n the x_goal of pair m - n.
 template <int DIM>
-__global__ void tt_fourier_kernel(const float* __restrict__ xp, int64_t n,
+__global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict__ xp, int64_t n,
                                   const float* __restrict__ Btab, const int32_t* __restrict__ env,
                                   int32_t n_env, float* __restrict__ phi) {
   const int64_t M = 2 * n, plane = M * 256;
@@ -103,50 +103,66 @@ __global__ void tt_fourier_kernel(const float* __restrict__ xp, int64_t n,
 }
 
 // ---------------------------------------------------------------- act_laplace (:675-691)
+// Elementwise over planes with 16-byte accesses: a thread owns 4 consecutive features of one
+// point (W is 128 or 256, a multiple of 4), so every plane access is one dwordx4 per lane.
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
 // y (R, M, W): GEMM output; plane 0 gets the bias (kept in place as the saved
 // pre-activation).  ACT: h = softplus10(y), J' = σJ, L' = σ'J² + σL (σ = σ(10y), σ' = 10σ(1-σ)).
 // RES: the residual branch (:744, :828) res (R, M, W) is added to every plane first (and
 // the sum kept in y).
 template <int NDIR, bool ACT, bool RES>
-__global__ void tt_act_fwd_kernel(float* __restrict__ y, float* __restrict__ h,
+__global__ __launch_bounds__(256) void tt_act_fwd_kernel(float* __restrict__ y, float* __restrict__ h,
                                   const float* __restrict__ bias, const float* __restrict__ res,
                                   int64_t M, int W) {
   const int64_t plane = M * W;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < plane;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float v = y[i] + bias[i % W] + (RES ? res[i] : 0.f);
-    y[i] = v;
+  for (int64_t i = 4 * (blockIdx.x * (int64_t)blockDim.x + threadIdx.x); i < plane;
+       i += 4 * (int64_t)gridDim.x * blockDim.x) {
+    f4 v = ld4(y + i) + ld4(bias + i % W);
+    if (RES) v += ld4(res + i);
+    st4(y + i, v);
     if (!ACT) continue;
-    const float s = sig10(v), ds = SCALE * s * (1.f - s);
-    h[i] = softplus10(v);
+    f4 s, ds, hv;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      s[c] = sig10(v[c]);
+      ds[c] = SCALE * s[c] * (1.f - s[c]);
+      hv[c] = softplus10(v[c]);
+    }
+    st4(h + i, hv);
 #pragma unroll
     for (int k = 0; k < NDIR; ++k) {
-      float J = y[(1 + k) * plane + i], L = y[(1 + NDIR + k) * plane + i];
+      const int64_t iJ = (1 + k) * plane + i, iL = (1 + NDIR + k) * plane + i;
+      f4 J = ld4(y + iJ), L = ld4(y + iL);
       if (RES) {
-        J += res[(1 + k) * plane + i];
-        L += res[(1 + NDIR + k) * plane + i];
-        y[(1 + k) * plane + i] = J;
-        y[(1 + NDIR + k) * plane + i] = L;
+        J += ld4(res + iJ);
+        L += ld4(res + iL);
+        st4(y + iJ, J);
+        st4(y + iL, L);
       }
-      h[(1 + k) * plane + i] = J * s;
-      h[(1 + NDIR + k) * plane + i] = fmaf(J * J, ds, L * s);
+      st4(h + iJ, J * s);
+      st4(h + iL, J * J * ds + L * s);
     }
   }
 }
 
 // Per-block column partial sums of a (rows, W) value -> partial[blockIdx][W]: the thread owns
-// column tid % W and rows tid / W + k·RB; the RB row groups are folded through LDS.
+// columns 4·(tid % (W/4)) .. +3 and rows tid / (W/4) + k·RB; the RB row groups are folded
+// through LDS in fixed order.
 template <int W>
-__device__ __forceinline__ void block_colsum(float acc, float* __restrict__ partial) {
-  constexpr int RB = 256 / W;
-  __shared__ float red[256];
+__device__ __forceinline__ void block_colsum(f4 acc, float* __restrict__ partial) {
+  constexpr int TPR = W / 4, RB = 256 / TPR;
+  __shared__ f4 red[256];
   red[threadIdx.x] = acc;
   __syncthreads();
-  if (threadIdx.x < W) {
-    float s = 0.f;
+  if (threadIdx.x < TPR) {
+    f4 s = red[threadIdx.x];
 #pragma unroll
-    for (int r = 0; r < RB; ++r) s += red[r * W + threadIdx.x];
-    partial[blockIdx.x * W + threadIdx.x] = s;
+    for (int r = 1; r < RB; ++r) s += red[r * TPR + threadIdx.x];
+    st4(partial + blockIdx.x * W + 4 * threadIdx.x, s);
   }
 }
 
@@ -158,48 +174,78 @@ template <int NDIR, int W, bool ACT>
 __global__ __launch_bounds__(256) void tt_act_bwd_kernel(const float* __restrict__ y,
                                                          float* __restrict__ g, int64_t M,
                                                          float* __restrict__ partial) {
-  constexpr int RB = 256 / W;
+  constexpr int TPR = W / 4, RB = 256 / TPR;
   const int64_t plane = M * W;
-  const int j = threadIdx.x % W;
-  float acc = 0.f;
-  for (int64_t m = blockIdx.x * RB + threadIdx.x / W; m < M; m += (int64_t)gridDim.x * RB) {
+  const int j = 4 * (threadIdx.x % TPR);
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t m = blockIdx.x * RB + threadIdx.x / TPR; m < M; m += (int64_t)gridDim.x * RB) {
     const int64_t i = m * W + j;
     if (!ACT) {
-      acc += g[i];
+      acc += ld4(g + i);
       continue;
     }
-    const float v = y[i];
-    const float s = sig10(v), ds = SCALE * s * (1.f - s), dds = SCALE * ds * (1.f - 2.f * s);
-    float gy = g[i] * s;
+    const f4 v = ld4(y + i);
+    f4 s, ds, dds;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      s[c] = sig10(v[c]);
+      ds[c] = SCALE * s[c] * (1.f - s[c]);
+      dds[c] = SCALE * ds[c] * (1.f - 2.f * s[c]);
+    }
+    f4 gy = ld4(g + i) * s;
 #pragma unroll
     for (int k = 0; k < NDIR; ++k) {
       const int64_t iJ = (1 + k) * plane + i, iL = (1 + NDIR + k) * plane + i;
-      const float J = y[iJ], L = y[iL], gJ = g[iJ], gL = g[iL];
-      gy += gJ * J * ds + gL * fmaf(J * J, dds, L * ds);
-      g[iJ] = fmaf(gJ, s, 2.f * gL * J * ds);
-      g[iL] = gL * s;
+      const f4 J = ld4(y + iJ), L = ld4(y + iL), gJ = ld4(g + iJ), gL = ld4(g + iL);
+      gy += gJ * J * ds + gL * (J * J * dds + L * ds);
+      st4(g + iJ, gJ * s + 2.f * gL * J * ds);
+      st4(g + iL, gL * s);
     }
-    g[i] = gy;
+    st4(g + i, gy);
     acc += gy;
   }
   block_colsum<W>(acc, partial);
 }
 
-// out[j] (+)= Σ_b partial[b][j] in block order (deterministic)
-__global__ void reduce_kernel(const float* __restrict__ partial, int nb, int W,
-                              float* __restrict__ out, int accumulate) {
-  for (int j = threadIdx.x; j < W; j += blockDim.x) {
-    float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += partial[b * W + j];
+// out[j] (+)= Σ_b partial[b][j], deterministic: workgroup x owns columns 64x..64x+63 (one per
+// lane, coalesced rows); wave w sums the rows b ≡ w (mod 4) in order, 4 loads in flight; the
+// four wave sums are combined in fixed order through LDS.
+__global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ partial, int nb,
+                                                     int W, float* __restrict__ out,
+                                                     int accumulate) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < W) {
+    int b = w;
+    for (; b + 12 < nb; b += 16) {
+      s0 += partial[(int64_t)b * W + j];
+      s1 += partial[(int64_t)(b + 4) * W + j];
+      s2 += partial[(int64_t)(b + 8) * W + j];
+      s3 += partial[(int64_t)(b + 12) * W + j];
+    }
+    for (; b < nb; b += 4) s0 += partial[(int64_t)b * W + j];
+  }
+  __shared__ float red[4][64];
+  red[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && j < W) {
+    const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
     out[j] = accumulate ? out[j] + s : s;
   }
+}
+
+void launch_reduce(const float* partial, int nb, int W, float* out, int accumulate,
+                   hipStream_t stream) {
+  hipLaunchKernelGGL(reduce_kernel, dim3((W + 63) / 64), dim3(256), 0, stream, partial, nb, W,
+                     out, accumulate);
 }
 
 // ---------------------------------------------------------------- start/goal merge (:761-811)
 // z (1 + 2 DIM, 2n, 128) encoder output planes -> u (1 + 4 DIM, n, 256) generator planes
 // [value | ∂xs (DIM) | ∂xg (DIM) | ∂²xs (DIM) | ∂²xg (DIM)], features [max-part | min-part].
 template <int DIM>
-__global__ void tt_merge_fwd_kernel(const float* __restrict__ z, int64_t n,
+__global__ __launch_bounds__(256) void tt_merge_fwd_kernel(const float* __restrict__ z, int64_t n,
                                     float* __restrict__ u) {
   const int64_t pz = 2 * n * H, pu = n * 256;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * H;
@@ -231,7 +277,7 @@ __global__ void tt_merge_fwd_kernel(const float* __restrict__ z, int64_t n,
 
 // Adjoint of the merge: gu (1 + 4 DIM, n, 256) -> gz (1 + 2 DIM, 2n, 128).
 template <int DIM>
-__global__ void tt_merge_bwd_kernel(const float* __restrict__ z, const float* __restrict__ gu,
+__global__ __launch_bounds__(256) void tt_merge_bwd_kernel(const float* __restrict__ z, const float* __restrict__ gu,
                                     int64_t n, float* __restrict__ gz) {
   const int64_t pz = 2 * n * H, pu = n * 256;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * H;
@@ -439,7 +485,7 @@ int pntf_tt_act_fwd(int ndir, float* y, float* h, const float* bias, const float
       (m > 0 && (!y || !bias || (act && !h))) || (res && !act))
     return fail("pntf_tt_act_fwd: bad arguments");
   if (m == 0) return PNTF_OK;
-  const dim3 g(grid_1d(m * w)), b(256);
+  const dim3 g(grid_1d(m * w / 4)), b(256);
 #define PNTF_ACT_FWD(N)                                                                   \
   if (res) hipLaunchKernelGGL((tt_act_fwd_kernel<N, true, true>), g, b, 0, stream, y, h, bias, \
                               res, m, w);                                                 \
@@ -459,7 +505,7 @@ int pntf_tt_act_bwd(int ndir, const float* y, float* g, int64_t m, int w, int ac
   if ((ndir != 3 && ndir != 6 && ndir != 12) || m < 0 || (w != 128 && w != 256) || !gbias ||
       !partial || (m > 0 && (!g || (act && !y))))
     return fail("pntf_tt_act_bwd: bad arguments");
-  const int nb = nb_for(m / (256 / w));
+  const int nb = nb_for(m / (1024 / w));
   const dim3 gr(nb), b(256);
 #define PNTF_ACT_BWD(N, W)                                                                 \
   if (act) hipLaunchKernelGGL((tt_act_bwd_kernel<N, W, true>), gr, b, 0, stream, y, g, m,     \
@@ -475,8 +521,7 @@ int pntf_tt_act_bwd(int ndir, const float* y, float* g, int64_t m, int w, int ac
     else { PNTF_ACT_BWD(12, 256) }
   }
 #undef PNTF_ACT_BWD
-  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, stream, partial, nb, w, gbias,
-                     accumulate);
+  launch_reduce(partial, nb, w, gbias, accumulate, stream);
   return check_launch("tt_act_bwd_kernel");
 }
 
@@ -521,9 +566,8 @@ int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const f
     else PNTF_HEAD(6, false);
   }
 #undef PNTF_HEAD
-  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(256), 0, stream, partial, nb, 128, gw4, 0);
-  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(64), 0, stream, partial + (int64_t)nb * 128,
-                     nb, 1, gb4, 0);
+  launch_reduce(partial, nb, 128, gw4, 0, stream);
+  launch_reduce(partial + (int64_t)nb * 128, nb, 1, gb4, 0, stream);
   return check_launch("tt_head_loss_kernel");
 }
 

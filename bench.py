@@ -236,7 +236,30 @@ def extras(packed, dev):
         ms = timeit(run1, reps=2)
         out["gib_plan_q1_ms_per_step_" + sched] = ms / 100.0
     out.update(train_extras(dev))
+    out.update(mesh_extras(dev))
     return out
+
+
+def mesh_extras(dev, n=1 << 20, t=20000, reps=3):
+    """Speed-sample generator distance query (dataprocessing/speed_sampling_gpu.py:325-336):
+    n sampled points against a t-triangle synthetic obstacle mesh (Gibson meshes are
+    10^3..10^5 triangles).  VALU-bound; reported as point-triangle tests per second."""
+    g = torch.Generator(device="cpu").manual_seed(9)
+    tris = ((torch.rand(t, 1, 3, generator=g) - 0.5) * 0.8
+            + torch.randn(t, 3, 3, generator=g) * 0.02).to(dev)
+    pts = (torch.rand(n, 3, generator=g) - 0.5).to(dev)
+    ops.point_mesh_distance(pts, tris)
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        ops.point_mesh_distance(pts, tris)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / reps
+    return {"mesh_distance_1M_pts_20k_tris_ms": ms,
+            "mesh_distance_point_tri_tests_per_s": n * t / (ms * 1e-3)}
 
 
 TRAIN_FLOP_PER_PAIR = 3 * 14_286_848   # Taylor forward + 2x for the adjoint (GEMM MACs x 2)
@@ -284,5 +307,9 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--train-only":
         torch.cuda.set_device(0)
         print(json.dumps(train_extras(torch.device("cuda", 0))), flush=True)
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--mesh-only":
+        torch.cuda.set_device(0)
+        print(json.dumps(mesh_extras(torch.device("cuda", 0))), flush=True)
         sys.exit(0)
     main()

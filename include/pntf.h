@@ -188,6 +188,18 @@ int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const f
 int pntf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                float beta2, float eps, float weight_decay, int64_t step, hipStream_t stream);
 
+/* ---- Speed-sample generator (pntf_mesh.hip) ---------------------- */
+
+/* Unsigned distance from each of n points `pts` (n, 3) to the triangle mesh `tris` (t, 3, 3)
+ * (= v_obs[f_obs], dataprocessing/speed_sampling_gpu.py:386-388) -> `dist` (n).  Replaces
+ * point_obstacle_distance (speed_sampling_gpu.py:325-336), i.e. bvh_distance_queries.BVH()
+ * (squared closest-point distances) followed by torch.sqrt.  `chunks` splits the triangle
+ * range over the grid (0 = auto, pntf_mesh_chunks); any value gives the same bits. */
+int pntf_point_mesh_distance(const float* pts, int64_t n, const float* tris, int64_t t,
+                             float* dist, int chunks, hipStream_t stream);
+int pntf_mesh_chunks(int64_t n, int64_t t);
+const char* pntf_mesh_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

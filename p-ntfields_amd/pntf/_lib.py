@@ -71,6 +71,11 @@ SIGNATURES = {
                                          _c_void_p]),
     "pntf_adamw": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32,
                                   _f32, _f32, _f32, _i64, _c_void_p]),
+    # speed-sample generator (pntf_mesh.hip)
+    "pntf_point_mesh_distance": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _c_void_p,
+                                                ctypes.c_int, _c_void_p]),
+    "pntf_mesh_chunks": (ctypes.c_int, [_i64, _i64]),
+    "pntf_mesh_last_error": (ctypes.c_char_p, []),
 }
 
 _lib = None
@@ -103,7 +108,12 @@ def load():
 def check(status, what):
     if status != 0:
         lib = load()
-        err = (lib.pntf_tt_last_error() if what.startswith(("pntf_tt_", "pntf_adamw"))
-               else lib.pntf_last_error()).decode()
+        if what.startswith(("pntf_tt_", "pntf_adamw")):
+            err = lib.pntf_tt_last_error()
+        elif what.startswith("pntf_point_mesh"):
+            err = lib.pntf_mesh_last_error()
+        else:
+            err = lib.pntf_last_error()
+        err = err.decode()
         raise PntfError("%s failed: %s (%s)" % (
             what, lib.pntf_status_string(status).decode(), err))

@@ -13,7 +13,7 @@ from ._lib import GRAD_BACKGRAD_COMPAT, GRAD_EXACT, PntfError, check
 
 __all__ = ["GRAD_EXACT", "GRAD_BACKGRAD_COMPAT", "PntfError", "pack_weights", "tau",
            "tau_grad", "path_velocity", "speed", "travel_time", "plan", "eikonal_residual",
-           "device_sum", "packed_floats", "workspace_bytes"]
+           "device_sum", "packed_floats", "workspace_bytes", "point_mesh_distance"]
 
 _ws_cache = {}
 
@@ -228,4 +228,29 @@ def device_sum(x):
     x = x.detach().to(torch.float32).contiguous().reshape(-1)
     out = torch.empty((), dtype=torch.float64, device=x.device)
     check(lib.pntf_sum(_vp(x), x.numel(), _vp(out), _stream(x.device)), "pntf_sum")
+    return out
+
+
+def point_mesh_distance(pts, tris, chunks=0):
+    """Unsigned distance (n,) from pts (n, 3) to the triangle mesh tris (t, 3, 3) on the HIP
+    kernel (pntf_point_mesh_distance) — what point_obstacle_distance returns
+    (dataprocessing/speed_sampling_gpu.py:325-336: bvh_distance_queries, then sqrt).
+    `chunks` = 0 picks the triangle split automatically; every value gives the same bits."""
+    _require_device(pts, "pts")
+    _require_device(tris, "tris")
+    if pts.dim() != 2 or pts.shape[1] != 3:
+        raise PntfError("pts must be (n, 3), got %s" % (tuple(pts.shape),))
+    tris = tris.reshape(-1, 3, 3) if tris.dim() == 4 and tris.shape[0] == 1 else tris
+    if tris.dim() != 3 or tuple(tris.shape[1:]) != (3, 3):
+        raise PntfError("tris must be (t, 3, 3) or (1, t, 3, 3), got %s" % (tuple(tris.shape),))
+    if pts.device != tris.device:
+        raise PntfError("pts and tris must be on the same device")
+    pts = pts.detach().to(torch.float32).contiguous()
+    tris = tris.detach().to(torch.float32).contiguous()
+    out = torch.empty(pts.shape[0], dtype=torch.float32, device=pts.device)
+    if pts.shape[0] == 0:
+        return out
+    check(_lib.load().pntf_point_mesh_distance(_vp(pts), pts.shape[0], _vp(tris), tris.shape[0],
+                                                _vp(out), int(chunks), _stream(pts.device)),
+          "pntf_point_mesh_distance")
     return out

@@ -9,17 +9,19 @@
 // MI355X design: the meshes here are the scaled Gibson obstacle meshes (10^3..10^5
 // triangles) and a sampling round queries 8·numsamples points, so the work is a dense
 // (points x triangles) min-reduction, VALU-bound, not a pointer-chasing tree walk.  Each
-// workgroup owns 256 points (one per lane, in registers) and a contiguous chunk of
-// triangles, which it stages through LDS 256 at a time; every lane then reads the same
-// triangle (LDS broadcast, conflict-free).  When the point grid alone cannot fill 256 CUs
+// workgroup owns 512 points (two per lane, in registers) and a contiguous chunk of
+// triangles, which it stages through LDS 256 at a time as precomputed records (edges,
+// inverse edge lengths, unit normal, in-plane edge normals); every lane then reads the same
+// record (LDS broadcast, conflict-free) and runs a branch-free distance (no divergence).  When the point grid alone cannot fill 256 CUs
 // the triangle range is split over grid.y and the chunks combine with a global unsigned
 // atomic min on the fp32 bit pattern of d^2 (order-preserving for d^2 >= 0, so the result
 // is the exact minimum, independent of chunk order); a finalize pass takes the sqrt.
 //
-// Closest point on a triangle: the region test of Ericson, "Real-Time Collision Detection"
-// §5.1.5 (the algorithm bvh_distance_queries' device code uses), restated in fp32.
-// Degenerate (sin^2 of the angle at vertex a <= 1e-12) triangles whose closest point falls
-// in the interior region fall back to the nearest of their three edges.
+// Closest point on a triangle: the Voronoi regions of Ericson, "Real-Time Collision
+// Detection" §5.1.5 (the algorithm bvh_distance_queries' device code uses) in a branch-free
+// form — plane distance when the projection is inside, else the nearest edge; the oracle
+// (oracle/mesh_oracle.py) keeps Ericson's branchy form, an independent formulation.
+// Degenerate triangles (sin^2 of the angle at vertex a <= 1e-12) use the nearest edge.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -52,105 +54,105 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
   return fmaf(ax, bx, fmaf(ay, by, az * bz));
 }
 
-// squared distance from p to segment [a, a + e]
-__device__ __forceinline__ float seg_d2(float px, float py, float pz, float ax, float ay,
-                                        float az, float ex, float ey, float ez) {
-  const float qx = px - ax, qy = py - ay, qz = pz - az;
-  const float ee = dot3(ex, ey, ez, ex, ey, ez);
-  float t = ee > 0.f ? dot3(qx, qy, qz, ex, ey, ez) / ee : 0.f;
-  t = fminf(fmaxf(t, 0.f), 1.f);
-  const float rx = qx - t * ex, ry = qy - t * ey, rz = qz - t * ez;
-  return dot3(rx, ry, rz, rx, ry, rz);
-}
+// Per-triangle record staged in LDS (8 float4, built once per tile by one lane each):
+//   [0] a, 1/|ab|^2   [1] ab, 1/|ac|^2   [2] ac, 1/|bc|^2   [3] bc, flat
+//   [4] n^ (unit normal)   [5] m_ab = n^ x ab   [6] m_ac = ac x n^   [7] m_bc = n^ x bc
+// m_* are in-plane edge normals pointing into the triangle; `flat` = 1 for a (near-)zero-area
+// triangle (sin^2 of the angle at a <= 1e-12), whose distance is then its nearest edge.
+constexpr int REC = 8;
 
-// Ericson §5.1.5 ClosestPtPointTriangle; returns |p - closest|^2.
-__device__ __forceinline__ float tri_d2(float px, float py, float pz, const float* __restrict__ t) {
+__device__ __forceinline__ void build_record(const float* __restrict__ t, float4* __restrict__ r) {
   const float ax = t[0], ay = t[1], az = t[2];
-  const float bx = t[3], by = t[4], bz = t[5];
-  const float cx = t[6], cy = t[7], cz = t[8];
-  const float abx = bx - ax, aby = by - ay, abz = bz - az;
-  const float acx = cx - ax, acy = cy - ay, acz = cz - az;
-  const float apx = px - ax, apy = py - ay, apz = pz - az;
-  const float d1 = dot3(abx, aby, abz, apx, apy, apz);
-  const float d2 = dot3(acx, acy, acz, apx, apy, apz);
-  float qx, qy, qz;
-  if (d1 <= 0.f && d2 <= 0.f) {
-    qx = ax; qy = ay; qz = az;
-  } else {
-    const float bpx = px - bx, bpy = py - by, bpz = pz - bz;
-    const float d3 = dot3(abx, aby, abz, bpx, bpy, bpz);
-    const float d4 = dot3(acx, acy, acz, bpx, bpy, bpz);
-    const float cpx = px - cx, cpy = py - cy, cpz = pz - cz;
-    const float d5 = dot3(abx, aby, abz, cpx, cpy, cpz);
-    const float d6 = dot3(acx, acy, acz, cpx, cpy, cpz);
-    const float vc = d1 * d4 - d3 * d2;
-    const float vb = d5 * d2 - d1 * d6;
-    const float va = d3 * d6 - d5 * d4;
-    if (d3 >= 0.f && d4 <= d3) {
-      qx = bx; qy = by; qz = bz;
-    } else if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
-      const float v = d1 / (d1 - d3);
-      qx = ax + v * abx; qy = ay + v * aby; qz = az + v * abz;
-    } else if (d6 >= 0.f && d5 <= d6) {
-      qx = cx; qy = cy; qz = cz;
-    } else if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
-      const float w = d2 / (d2 - d6);
-      qx = ax + w * acx; qy = ay + w * acy; qz = az + w * acz;
-    } else if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
-      const float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-      qx = bx + w * (cx - bx); qy = by + w * (cy - by); qz = bz + w * (cz - bz);
-    } else {
-      // interior region; a (near-)zero-area triangle, sin^2(angle at a) <= 1e-12, makes
-      // va + vb + vc ill-conditioned: take its nearest edge instead
-      const float nx = aby * acz - abz * acy, ny = abz * acx - abx * acz,
-                  nz = abx * acy - aby * acx;
-      const float s = va + vb + vc;
-      if (!(s > 0.f) || dot3(nx, ny, nz, nx, ny, nz) <=
-                            1e-12f * dot3(abx, aby, abz, abx, aby, abz) *
-                                dot3(acx, acy, acz, acx, acy, acz)) {
-        float m = seg_d2(px, py, pz, ax, ay, az, abx, aby, abz);
-        m = fminf(m, seg_d2(px, py, pz, ax, ay, az, acx, acy, acz));
-        return fminf(m, seg_d2(px, py, pz, bx, by, bz, cx - bx, cy - by, cz - bz));
-      }
-      const float denom = 1.f / s;
-      const float v = vb * denom, w = vc * denom;
-      qx = ax + abx * v + acx * w; qy = ay + aby * v + acy * w; qz = az + abz * v + acz * w;
-    }
-  }
-  const float rx = px - qx, ry = py - qy, rz = pz - qz;
+  const float abx = t[3] - ax, aby = t[4] - ay, abz = t[5] - az;
+  const float acx = t[6] - ax, acy = t[7] - ay, acz = t[8] - az;
+  const float bcx = t[6] - t[3], bcy = t[7] - t[4], bcz = t[8] - t[5];
+  const float ab2 = dot3(abx, aby, abz, abx, aby, abz);
+  const float ac2 = dot3(acx, acy, acz, acx, acy, acz);
+  const float bc2 = dot3(bcx, bcy, bcz, bcx, bcy, bcz);
+  float nx = aby * acz - abz * acy, ny = abz * acx - abx * acz, nz = abx * acy - aby * acx;
+  const float nn = dot3(nx, ny, nz, nx, ny, nz);
+  const bool flat = !(nn > 1e-12f * ab2 * ac2);
+  const float inv = flat ? 0.f : 1.f / sqrtf(nn);
+  nx *= inv; ny *= inv; nz *= inv;
+  r[0] = make_float4(ax, ay, az, ab2 > 0.f ? 1.f / ab2 : 0.f);
+  r[1] = make_float4(abx, aby, abz, ac2 > 0.f ? 1.f / ac2 : 0.f);
+  r[2] = make_float4(acx, acy, acz, bc2 > 0.f ? 1.f / bc2 : 0.f);
+  r[3] = make_float4(bcx, bcy, bcz, flat ? 1.f : 0.f);
+  r[4] = make_float4(nx, ny, nz, 0.f);
+  r[5] = make_float4(ny * abz - nz * aby, nz * abx - nx * abz, nx * aby - ny * abx, 0.f);
+  r[6] = make_float4(acy * nz - acz * ny, acz * nx - acx * nz, acx * ny - acy * nx, 0.f);
+  r[7] = make_float4(ny * bcz - nz * bcy, nz * bcx - nx * bcz, nx * bcy - ny * bcx, 0.f);
+}
+
+// squared distance from q (= p - origin) to the segment origin + [0,1]·e, 1/|e|^2 = ie
+__device__ __forceinline__ float seg_d2(float qx, float qy, float qz, float4 e, float ie) {
+  const float tt = fminf(fmaxf(dot3(qx, qy, qz, e.x, e.y, e.z) * ie, 0.f), 1.f);
+  const float rx = fmaf(-tt, e.x, qx), ry = fmaf(-tt, e.y, qy), rz = fmaf(-tt, e.z, qz);
   return dot3(rx, ry, rz, rx, ry, rz);
 }
 
-// grid (ceil(n/256), n_chunks); chunk y covers triangles [y*per, min(t,(y+1)*per)).
+// Branch-free |p - closest point of the triangle|^2: if p projects inside the triangle the
+// distance is the plane distance, otherwise the nearest of the three edges (exactly the
+// Voronoi regions of Ericson §5.1.5, evaluated without divergence: every lane of a wave
+// runs the same instructions whatever region its point falls in).
+__device__ __forceinline__ float tri_d2(float px, float py, float pz,
+                                        const float4* __restrict__ r) {
+  const float4 a = r[0], ab = r[1], ac = r[2], bc = r[3];
+  const float qx = px - a.x, qy = py - a.y, qz = pz - a.z;           // p - a
+  const float bx = qx - ab.x, by = qy - ab.y, bz = qz - ab.z;        // p - b
+  float e = fminf(seg_d2(qx, qy, qz, ab, a.w), seg_d2(qx, qy, qz, ac, ab.w));
+  e = fminf(e, seg_d2(bx, by, bz, bc, ac.w));
+  const float4 n = r[4], m0 = r[5], m1 = r[6], m2 = r[7];
+  const float h = dot3(qx, qy, qz, n.x, n.y, n.z);
+  const bool inside = dot3(qx, qy, qz, m0.x, m0.y, m0.z) >= 0.f &&
+                      dot3(qx, qy, qz, m1.x, m1.y, m1.z) >= 0.f &&
+                      dot3(bx, by, bz, m2.x, m2.y, m2.z) >= 0.f && bc.w == 0.f;
+  return inside ? fminf(h * h, e) : e;
+}
+
+// grid (ceil(n/PPW), n_chunks); chunk y covers triangles [y*per, min(t,(y+1)*per)).  Each
+// lane owns PTS points (PPW = 256·PTS per workgroup), so one LDS record read serves PTS tests.
 // SPLIT: combine through atomicMin on d^2 bits in `acc`; else write sqrt(d^2) to `dist`.
+constexpr int PTS = 2;
+constexpr int PPW = BLOCK * PTS;
+
 template <bool SPLIT>
 __global__ __launch_bounds__(BLOCK) void mesh_distance_kernel(
     const float* __restrict__ pts, int64_t n, const float* __restrict__ tris, int64_t t,
     int64_t per, float* __restrict__ dist, unsigned int* __restrict__ acc) {
-  __shared__ float s_tri[BLOCK * 9];
-  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const bool live = i < n;
-  float px = 0.f, py = 0.f, pz = 0.f;
-  if (live) {
-    px = pts[3 * i]; py = pts[3 * i + 1]; pz = pts[3 * i + 2];
+  __shared__ float4 s_rec[BLOCK * REC];
+  float px[PTS], py[PTS], pz[PTS], best[PTS];
+#pragma unroll
+  for (int k = 0; k < PTS; ++k) {
+    const int64_t i = (int64_t)blockIdx.x * PPW + k * BLOCK + threadIdx.x;
+    px[k] = py[k] = pz[k] = 0.f;
+    if (i < n) {
+      px[k] = pts[3 * i]; py[k] = pts[3 * i + 1]; pz[k] = pts[3 * i + 2];
+    }
+    best[k] = INFINITY;
   }
   const int64_t t0 = (int64_t)blockIdx.y * per;
   const int64_t t1 = t0 + per < t ? t0 + per : t;
-  float best = INFINITY;
   for (int64_t base = t0; base < t1; base += BLOCK) {
     const int cnt = (int)(t1 - base < BLOCK ? t1 - base : BLOCK);
     __syncthreads();
-    // coalesced: the tile is cnt*9 contiguous floats
-    const float* src = tris + base * 9;
-    for (int k = threadIdx.x; k < cnt * 9; k += BLOCK) s_tri[k] = src[k];
+    if (threadIdx.x < cnt) build_record(tris + (base + threadIdx.x) * 9, s_rec + REC * threadIdx.x);
     __syncthreads();
-    for (int j = 0; j < cnt; ++j) best = fminf(best, tri_d2(px, py, pz, s_tri + 9 * j));
+    for (int j = 0; j < cnt; ++j) {
+#pragma unroll
+      for (int k = 0; k < PTS; ++k)
+        best[k] = fminf(best[k], tri_d2(px[k], py[k], pz[k], s_rec + REC * j));
+    }
   }
-  if (!live) return;
-  if (SPLIT)
-    atomicMin(acc + i, __float_as_uint(best));
-  else
-    dist[i] = sqrtf(best);
+#pragma unroll
+  for (int k = 0; k < PTS; ++k) {
+    const int64_t i = (int64_t)blockIdx.x * PPW + k * BLOCK + threadIdx.x;
+    if (i >= n) continue;
+    if (SPLIT)
+      atomicMin(acc + i, __float_as_uint(best[k]));
+    else
+      dist[i] = sqrtf(best[k]);
+  }
 }
 
 __global__ void fill_inf_kernel(unsigned int* __restrict__ acc, int64_t n) {
@@ -171,7 +173,7 @@ const char* pntf_mesh_last_error(void) { return g_err; }
 
 int pntf_mesh_chunks(int64_t n, int64_t t) {
   if (n <= 0 || t <= 0) return 1;
-  const int64_t gx = (n + BLOCK - 1) / BLOCK;
+  const int64_t gx = (n + PPW - 1) / PPW;
   const int64_t tiles = (t + BLOCK - 1) / BLOCK;
   int64_t c = (TARGET_WG + gx - 1) / gx;
   if (c > tiles) c = tiles;
@@ -185,7 +187,7 @@ int pntf_point_mesh_distance(const float* pts, int64_t n, const float* tris, int
     return fail("pntf_point_mesh_distance: bad arguments");
   if (n == 0) return PNTF_OK;
   if (t == 0) return fail("pntf_point_mesh_distance: empty mesh");
-  if ((n + BLOCK - 1) / BLOCK > 0x7fffffff)
+  if ((n + PPW - 1) / PPW > 0x7fffffff)
     return fail("pntf_point_mesh_distance: too many points");
   if (chunks <= 0) chunks = pntf_mesh_chunks(n, t);
   if (chunks > 65535) return fail("pntf_point_mesh_distance: chunks > 65535");
@@ -193,7 +195,7 @@ int pntf_point_mesh_distance(const float* pts, int64_t n, const float* tris, int
   int64_t per = (t + chunks - 1) / chunks;
   per = (per + BLOCK - 1) / BLOCK * BLOCK;
   const int64_t c = (t + per - 1) / per;
-  const dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK), (unsigned)c);
+  const dim3 grid((unsigned)((n + PPW - 1) / PPW), (unsigned)c);
   if (c == 1) {
     hipLaunchKernelGGL(mesh_distance_kernel<false>, grid, dim3(BLOCK), 0, stream, pts, n, tris,
                        t, per, dist, nullptr);

@@ -9,7 +9,7 @@
 // MI355X design: the meshes here are the scaled Gibson obstacle meshes (10^3..10^5
 // triangles) and a sampling round queries 8·numsamples points, so the work is a dense
 // (points x triangles) min-reduction, VALU-bound, not a pointer-chasing tree walk.  Each
-// workgroup owns 512 points (two per lane, in registers) and a contiguous chunk of
+// workgroup owns 1024 points (four per lane, in registers) and a contiguous chunk of
 // triangles, which it stages through LDS 256 at a time as precomputed records (edges,
 // inverse edge lengths, unit normal, in-plane edge normals); every lane then reads the same
 // record (LDS broadcast, conflict-free) and runs a branch-free distance (no divergence).  When the point grid alone cannot fill 256 CUs
@@ -113,7 +113,7 @@ __device__ __forceinline__ float tri_d2(float px, float py, float pz,
 // grid (ceil(n/PPW), n_chunks); chunk y covers triangles [y*per, min(t,(y+1)*per)).  Each
 // lane owns PTS points (PPW = 256·PTS per workgroup), so one LDS record read serves PTS tests.
 // SPLIT: combine through atomicMin on d^2 bits in `acc`; else write sqrt(d^2) to `dist`.
-constexpr int PTS = 2;
+constexpr int PTS = 4;
 constexpr int PPW = BLOCK * PTS;
 
 template <bool SPLIT>

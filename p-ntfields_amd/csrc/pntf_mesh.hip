@@ -59,7 +59,8 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
 //   [4] n^ (unit normal)   [5] m_ab = n^ x ab   [6] m_ac = ac x n^   [7] m_bc = n^ x bc
 // m_* are in-plane edge normals pointing into the triangle; `flat` = 1 for a (near-)zero-area
 // triangle (sin^2 of the angle at a <= 1e-12), whose distance is then its nearest edge.
-constexpr int REC = 8;
+//   [8] triangle AABB min   [9] triangle AABB max   (tile culling, see the kernel)
+constexpr int REC = 10;
 
 __device__ __forceinline__ void build_record(const float* __restrict__ t, float4* __restrict__ r) {
   const float ax = t[0], ay = t[1], az = t[2];
@@ -82,6 +83,22 @@ __device__ __forceinline__ void build_record(const float* __restrict__ t, float4
   r[5] = make_float4(ny * abz - nz * aby, nz * abx - nx * abz, nx * aby - ny * abx, 0.f);
   r[6] = make_float4(acy * nz - acz * ny, acz * nx - acx * nz, acx * ny - acy * nx, 0.f);
   r[7] = make_float4(ny * bcz - nz * bcy, nz * bcx - nx * bcz, nx * bcy - ny * bcx, 0.f);
+  r[8] = make_float4(fminf(ax, fminf(t[3], t[6])), fminf(ay, fminf(t[4], t[7])),
+                     fminf(az, fminf(t[5], t[8])), 0.f);
+  r[9] = make_float4(fmaxf(ax, fmaxf(t[3], t[6])), fmaxf(ay, fmaxf(t[4], t[7])),
+                     fmaxf(az, fmaxf(t[5], t[8])), 0.f);
+}
+
+// workgroup-wide min / max of 256 lanes (4 waves): wave shuffles, then LDS
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  return v;
 }
 
 // squared distance from q (= p - origin) to the segment origin + [0,1]·e, 1/|e|^2 = ie
@@ -131,14 +148,61 @@ __global__ __launch_bounds__(BLOCK) void mesh_distance_kernel(
     }
     best[k] = INFINITY;
   }
+  // Tile culling: the workgroup's point box [lo, hi] and the largest current best d^2 of its
+  // points give a lower bound test per triangle — a triangle whose AABB is farther than
+  // that from the point box cannot lower any point's minimum, so skipping it changes no
+  // result bit.  It pays when a workgroup's points are compact (ops.point_mesh_distance
+  // feeds them in Morton order).  The test is workgroup-uniform: no divergence.
+  __shared__ float s_red[4][8];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float lo[3], hi[3];
+  {
+    float a[3] = {INFINITY, INFINITY, INFINITY}, b[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int k = 0; k < PTS; ++k) {
+      const int64_t i = (int64_t)blockIdx.x * PPW + k * BLOCK + threadIdx.x;
+      if (i < n) {
+        a[0] = fminf(a[0], px[k]); a[1] = fminf(a[1], py[k]); a[2] = fminf(a[2], pz[k]);
+        b[0] = fmaxf(b[0], px[k]); b[1] = fmaxf(b[1], py[k]); b[2] = fmaxf(b[2], pz[k]);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      a[d] = wave_min(a[d]);
+      b[d] = wave_max(b[d]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int d = 0; d < 3; ++d) { s_red[wave][d] = a[d]; s_red[wave][3 + d] = b[d]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      lo[d] = fminf(fminf(s_red[0][d], s_red[1][d]), fminf(s_red[2][d], s_red[3][d]));
+      hi[d] = fmaxf(fmaxf(s_red[0][3 + d], s_red[1][3 + d]),
+                    fmaxf(s_red[2][3 + d], s_red[3][3 + d]));
+    }
+  }
   const int64_t t0 = (int64_t)blockIdx.y * per;
   const int64_t t1 = t0 + per < t ? t0 + per : t;
   for (int64_t base = t0; base < t1; base += BLOCK) {
     const int cnt = (int)(t1 - base < BLOCK ? t1 - base : BLOCK);
+    float mb = -INFINITY;  // dead lanes keep best = inf but are excluded
+#pragma unroll
+    for (int k = 0; k < PTS; ++k)
+      if ((int64_t)blockIdx.x * PPW + k * BLOCK + threadIdx.x < n) mb = fmaxf(mb, best[k]);
+    mb = wave_max(mb);
     __syncthreads();
     if (threadIdx.x < cnt) build_record(tris + (base + threadIdx.x) * 9, s_rec + REC * threadIdx.x);
+    if (lane == 0) s_red[wave][6] = mb;
     __syncthreads();
+    const float bound = fmaxf(fmaxf(s_red[0][6], s_red[1][6]), fmaxf(s_red[2][6], s_red[3][6]));
     for (int j = 0; j < cnt; ++j) {
+      const float4 bmin = s_rec[REC * j + 8], bmax = s_rec[REC * j + 9];
+      const float gx = fmaxf(fmaxf(bmin.x - hi[0], lo[0] - bmax.x), 0.f);
+      const float gy = fmaxf(fmaxf(bmin.y - hi[1], lo[1] - bmax.y), 0.f);
+      const float gz = fmaxf(fmaxf(bmin.z - hi[2], lo[2] - bmax.z), 0.f);
+      if (dot3(gx, gy, gz, gx, gy, gz) > bound) continue;
 #pragma unroll
       for (int k = 0; k < PTS; ++k)
         best[k] = fminf(best[k], tri_d2(px[k], py[k], pz[k], s_rec + REC * j));

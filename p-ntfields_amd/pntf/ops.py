@@ -231,11 +231,30 @@ def device_sum(x):
     return out
 
 
-def point_mesh_distance(pts, tris, chunks=0):
+def _spread10(x):
+    x = (x | (x << 16)) & 0x030000FF
+    x = (x | (x << 8)) & 0x0300F00F
+    x = (x | (x << 4)) & 0x030C30C3
+    return (x | (x << 2)) & 0x09249249
+
+
+def morton_order(pts):
+    """Permutation putting pts (n, 3) in 30-bit Morton (Z-curve) order, on the device."""
+    lo = pts.min(0).values
+    span = (pts.max(0).values - lo).clamp_min(1e-30)
+    q = ((pts - lo) / span * 1023.0).long().clamp_(0, 1023)
+    code = _spread10(q[:, 0]) | (_spread10(q[:, 1]) << 1) | (_spread10(q[:, 2]) << 2)
+    return torch.argsort(code)
+
+
+def point_mesh_distance(pts, tris, chunks=0, order=None):
     """Unsigned distance (n,) from pts (n, 3) to the triangle mesh tris (t, 3, 3) on the HIP
     kernel (pntf_point_mesh_distance) — what point_obstacle_distance returns
     (dataprocessing/speed_sampling_gpu.py:325-336: bvh_distance_queries, then sqrt).
-    `chunks` = 0 picks the triangle split automatically; every value gives the same bits."""
+    `chunks` = 0 picks the triangle split automatically; every value gives the same bits.
+    `order` (default: n >= 4096) queries the points in Morton order, so each workgroup's
+    points are compact and the kernel's exact tile culling skips far triangles; results are
+    scattered back, bit-identical to the unordered query."""
     _require_device(pts, "pts")
     _require_device(tris, "tris")
     if pts.dim() != 2 or pts.shape[1] != 3:
@@ -250,7 +269,14 @@ def point_mesh_distance(pts, tris, chunks=0):
     out = torch.empty(pts.shape[0], dtype=torch.float32, device=pts.device)
     if pts.shape[0] == 0:
         return out
-    check(_lib.load().pntf_point_mesh_distance(_vp(pts), pts.shape[0], _vp(tris), tris.shape[0],
-                                                _vp(out), int(chunks), _stream(pts.device)),
+    if order is None:
+        order = pts.shape[0] >= 4096
+    perm = morton_order(pts) if order else None
+    q = pts[perm].contiguous() if order else pts
+    res = torch.empty_like(out) if order else out
+    check(_lib.load().pntf_point_mesh_distance(_vp(q), q.shape[0], _vp(tris), tris.shape[0],
+                                                _vp(res), int(chunks), _stream(pts.device)),
           "pntf_point_mesh_distance")
+    if order:
+        out[perm] = res
     return out

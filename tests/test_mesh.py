@@ -92,12 +92,29 @@ def test_hip_distance_matches_oracle(n, t):
 
 
 @pytest.mark.gpu
+def test_hip_distance_culling_on_large_sorted_query():
+    """Morton-ordered query with tile culling on a mesh of small clustered triangles:
+    matches the oracle and the unordered query bit for bit."""
+    from pntf import ops
+    rng = np.random.default_rng(8)
+    tris = random_mesh(rng, 4000, scale=0.01).astype(np.float32)
+    pts = rng.uniform(-0.5, 0.5, (20000, 3)).astype(np.float32)
+    P, T = torch.from_numpy(pts).cuda(), torch.from_numpy(tris).cuda()
+    a = ops.point_mesh_distance(P, T, order=True)
+    b = ops.point_mesh_distance(P, T, order=False)
+    assert torch.equal(a, b)
+    sub = rng.choice(20000, 1500, replace=False)
+    assert np.abs(a.cpu().numpy()[sub] - M.point_mesh_distance(pts[sub], tris)).max() < TOL
+
+
+@pytest.mark.gpu
 def test_hip_distance_bits_independent_of_triangle_split():
     from pntf import ops
     rng = np.random.default_rng(5)
     tris = torch.from_numpy(random_mesh(rng, 3000).astype(np.float32)).cuda()
     pts = torch.from_numpy(rng.uniform(-0.5, 0.5, (777, 3)).astype(np.float32)).cuda()
-    outs = [ops.point_mesh_distance(pts, tris, chunks=c) for c in (1, 2, 5, 12, 0)]
+    outs = [ops.point_mesh_distance(pts, tris, chunks=c, order=o) for c in (1, 2, 5, 12, 0)
+            for o in (False, True)]
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
 

@@ -2,18 +2,29 @@
 """Headline benchmark: (start, goal) τ+∇τ evaluations per second, Gibson 3D, 1M pairs per
 GPU (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--total-pairs T]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+`--gpus N` without a torch.distributed environment starts N rank processes itself
+(pntf/launch.py: one fresh interpreter per GPU, before anything touches the GPU); under
+torchrun the ranks come from the environment and WORLD_SIZE must equal N.
 
 One step = the fused HIP τ+∇τ kernel (exact reverse mode, = Model.gradient(NN.out)) over the
 rank's resident batch of synthetic Gibson-shaped pairs (10 environments, per-pair env id),
 followed for N > 1 by the RCCL all-gather of every rank's τ+∇τ rows (the multi-GPU exchange
-the north star names).  Weak scaling: every rank holds --pairs pairs.  Rank 0 prints one
-JSON line; `value` = all ranks' pairs / max-over-ranks wall time of the K timed steps.
+the north star names).  Weak scaling by default (--pairs per rank); --total-pairs T splits a
+fixed total over the ranks instead (strong scaling).  Rank 0 prints one JSON line; `value` =
+all ranks' pairs / max-over-ranks wall time of the K timed steps.
+
+After the timed steps every rank launches the kernel alone `--roofline-launches` times with
+a HIP event pair around each launch (on the stream it runs on): `roofline.achieved` is the
+algorithmic FLOP of one launch over the mean event-timed duration.  The CPU baseline (rank 0,
+N = 1) runs last, after every GPU leg.
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -26,136 +37,239 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as tdist  # noqa: E402
 
-from pntf import dist, ops, synth  # noqa: E402
+from pntf import dist, launch  # noqa: E402
 
 FLOP_PER_PAIR = 2_621_440          # 2 x (40*128^2 fwd + 40*128^2 bwd) GEMM MACs
 BYTES_PER_PAIR = 52                # 24 B in + 4 B tau + 24 B dtau (algorithmic HBM bytes)
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: Peak FP32 (matrix)
 METRIC = "(start,goal) tau+grad-tau evals/sec at batch=1M, Gibson 3D"
 UNIT = "pairs/s"
+HEADLINE_UNIT = "field_d3_k1"      # build unit of field_kernel<3, K_TAU_GRAD> (pntf/build.py)
 
 
-def cpu_baseline(seconds, n_chunk=4096):
-    """The fp32 numpy oracle (a restatement of the reference CPU path) on a bounded sample."""
-    from oracle import pntf_oracle as O
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    W = synth.make_weights(0)
-    xp = synth.make_pairs(n_chunk, 3, seed=2)
-    Bt = synth.make_B_table(10, 3)
-    env = synth.make_env_ids(n_chunk, 10)
-    O.tau_grad(W, xp[:256], Bt, env[:256], dtype=np.float32)      # warm-up
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        O.tau_grad(W, xp, Bt, env, dtype=np.float32)
-        done += n_chunk
-    el = time.perf_counter() - t0
-    return {"value": done / el, "unit": UNIT, "cores": cores, "kind": "port",
-            "sample": "%d pairs (%d-pair chunks, 10 envs) of the same synthetic workload, "
-                      "oracle/pntf_oracle.tau_grad in fp32 numpy, %.1f s" % (done, n_chunk, el)}
-
-
-def load_pmc(path, pairs):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/), scaled to
-    this launch's pair count; None when absent."""
-    try:
-        with open(path) as fh:
-            j = json.load(fh)
-        return float(j["hbm_bytes_per_pair"]) * pairs
-    except Exception:
-        return None
-
-
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pairs", type=int, default=1 << 20, help="pairs per GPU")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--pairs", type=int, default=1 << 20, help="pairs per GPU (weak scaling)")
+    ap.add_argument("--total-pairs", type=int, default=0,
+                    help="fixed total split over the GPUs (strong scaling)")
     ap.add_argument("--envs", type=int, default=10)
     ap.add_argument("--mode", choices=["exact", "compat"], default="exact")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--roofline-launches", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_tau_grad.json"))
-    args = ap.parse_args()
+    ap.add_argument("--rehearse", action="store_true",
+                    help="CPU/gloo rehearsal of the launcher, sharding, all-gather and "
+                         "max-over-ranks timing; no kernel runs and no metric is reported")
+    return ap.parse_args(argv)
 
-    rank, ws = dist.init()
-    _, _, local = dist.world()
+
+# ------------------------------------------------------------------------------ helpers
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(seconds, n_chunk=4096):
+    """The reference's CPU op sequence (torch Linear/Softplus/logsumexp + autograd.grad with
+    create_graph, oracle/torch_ref.py) on a bounded sample of the same workload."""
+    from oracle.torch_ref import TorchRef
+    from pntf import synth
+    threads = int(os.environ.get("OMP_NUM_THREADS", 0) or os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    ref = TorchRef(synth.make_weights(0))
+    xp = synth.make_pairs(n_chunk, 3, seed=2)
+    Bt = synth.make_B_table(10, 3)
+    env = synth.make_env_ids(n_chunk, 10)
+    ref.tau_grad(xp[:256], Bt, env[:256])                          # warm-up
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        ref.tau_grad(xp, Bt, env)
+        done += n_chunk
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": UNIT, "cores": torch.get_num_threads(),
+            "kind": "port", "cpu_model": cpu_model(),
+            "sample": "%d pairs (%d-pair batches, 10 envs, per-pair env id) of the same "
+                      "synthetic workload through oracle/torch_ref.py (the reference's torch "
+                      "CPU op sequence: NN.out + Model.gradient autograd, create_graph=True), "
+                      "fp32, %.1f s" % (done, n_chunk, el)}
+
+
+def pmc_traffic(path, pairs, unit_hash):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (profiles/), scaled to
+    this launch's pair count — only if it was collected from the kernel build that is loaded
+    now (same unit hash); otherwise (None, reason)."""
+    try:
+        with open(path) as fh:
+            j = json.load(fh)
+    except (OSError, ValueError) as e:
+        return None, "no PMC summary (%s)" % e
+    if j.get("unit_hash") != unit_hash:
+        return None, ("PMC summary %s was collected from build %s, loaded kernel is %s"
+                      % (os.path.basename(path), j.get("unit_hash"), unit_hash))
+    return float(j["hbm_bytes_per_pair"]) * pairs, "PMC %s (unit %s)" % (
+        os.path.basename(path), unit_hash)
+
+
+def timed(step, steps, warmup, ws, sync, dev_for_max):
+    """Warm-up, then exactly `steps` steps bracketed by barrier + sync; max over ranks."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if ws > 1:
+        tdist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if ws > 1:
+        tdist.barrier()
+    el = time.perf_counter() - t0
+    if ws > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev_for_max)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        el = float(tt.item())
+    return el
+
+
+def rank_share(args, rank, ws):
+    """(pairs on this rank, pairs over all ranks, scaling)."""
+    if args.total_pairs > 0:
+        lo, hi = dist.shard_range(args.total_pairs, rank, ws)
+        return hi - lo, args.total_pairs, "strong"
+    return args.pairs, args.pairs * ws, "weak"
+
+
+# ------------------------------------------------------------------------------ rehearsal
+def rehearse(args):
+    """Launcher rehearsal on CPU (gloo): the same rank layout, shard sizes, all-gather and
+    max-over-ranks timing as the GPU run, with a rank-tagged row block standing in for the
+    kernel output (nothing is computed, no metric is reported)."""
+    rank, ws = dist.init("gloo")
+    n, n_total, scaling = rank_share(args, rank, ws)
+    lo = dist.shard_range(n_total, rank, ws)[0] if scaling == "strong" else rank * n
+    rows = torch.arange(lo, lo + n, dtype=torch.float64).unsqueeze(1).repeat(1, 7)
+    rows[:, 1] = rank
+    res = {}
+
+    def step():
+        res["g"] = dist.all_gather_rows(rows, n_total)
+
+    el = timed(step, args.steps, args.warmup, ws, lambda: None, "cpu")
+    g = res["g"]
+    ok = bool(g.shape == (n_total, 7) and torch.equal(
+        g[:, 0], torch.arange(n_total, dtype=torch.float64)))
+    # C5-style planner paths, uneven query shards (q not a multiple of ws)
+    q = 37
+    ql, qh = dist.shard_range(q, rank, ws)
+    paths = torch.full((qh - ql, 5, 12), float(rank), dtype=torch.float32)
+    paths[:, 0, 0] = torch.arange(ql, qh, dtype=torch.float32)
+    gp = dist.all_gather_rows(paths, q)
+    ok = ok and bool(torch.equal(gp[:, 0, 0], torch.arange(q, dtype=torch.float32)))
+    if rank == 0:
+        print(json.dumps({"rehearsal": True, "n_gpus": ws, "world_size": tdist.get_world_size()
+                          if ws > 1 else 1, "steps": args.steps, "warmup": args.warmup,
+                          "scaling": scaling, "pairs_per_rank0": n, "global_batch": n_total,
+                          "gather_ok": ok, "max_over_ranks_s": el,
+                          "config": {"parallelism": "dp%d" % ws}}), flush=True)
+    if ws > 1:
+        tdist.barrier()
+        tdist.destroy_process_group()
+    return 0 if ok else 1
+
+
+# ------------------------------------------------------------------------------ GPU run
+def run(args):
+    from pntf import _lib, ops, synth
+    rank, ws, local = dist.world()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    dist.init("nccl", device=dev)
+    if ws > 1 and tdist.get_world_size() != args.gpus:
+        raise RuntimeError("RCCL world size %d != --gpus %d" % (tdist.get_world_size(),
+                                                                  args.gpus))
     mode = ops.GRAD_EXACT if args.mode == "exact" else ops.GRAD_BACKGRAD_COMPAT
 
     W = synth.make_weights(0)
     packed = ops.pack_weights([torch.from_numpy(v).to(dev) for v in W.values()])
-    n = args.pairs
-    n_total = n * ws
-    lo, hi = rank * n, (rank + 1) * n
+    n, n_total, scaling = rank_share(args, rank, ws)
+    lo = dist.shard_range(n_total, rank, ws)[0] if scaling == "strong" else rank * n
     xp = torch.from_numpy(synth.make_pairs(n, 3, seed=1000 + rank)).to(dev)
     Bt = torch.from_numpy(synth.make_B_table(args.envs, 3)).to(dev)
-    env = torch.from_numpy(synth.make_env_ids(n_total, args.envs)[lo:hi].copy()).to(dev)
+    env_all = synth.make_env_ids(n_total, args.envs)
+    env = torch.from_numpy(env_all[lo:lo + n].copy()).to(dev)
     gather = ws > 1 and not args.no_gather
+    res = {}
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record()
-        t, d = ops.tau_grad(packed, xp, Bt, env, dim=3, mode=mode)
-        if ev is not None:
-            ev[1].record()
+    def kernel():
+        return ops.tau_grad(packed, xp, Bt, env, dim=3, mode=mode)
+
+    def step():
+        t, d = kernel()
         if gather:
-            dist.all_gather_rows(torch.cat([t.unsqueeze(1), d], 1), n_total)
-        return t
+            res["g"] = dist.all_gather_rows(torch.cat([t.unsqueeze(1), d], 1), n_total)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    if ws > 1:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    if ws > 1:
-        tdist.barrier()
-    el = time.perf_counter() - t0
-    if ws > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        el = float(tt.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    el = timed(step, args.steps, args.warmup, ws, torch.cuda.synchronize, dev)
     value = n_total * args.steps / el
+
+    # roofline: per-launch HIP events on the launch stream (torch's current stream, which
+    # ops.* hands to the C ABI), kernel alone
+    stream = torch.cuda.current_stream(dev)
+    R = max(args.roofline_launches, args.steps)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(R)]
+    for a, b in evs:
+        a.record(stream)
+        kernel()
+        b.record(stream)
+    torch.cuda.synchronize()
+    kms = np.array([a.elapsed_time(b) for a, b in evs])
+    kern_ms = float(kms.mean())
     achieved = FLOP_PER_PAIR * n / (kern_ms * 1e-3) / 1e12
-    traffic = load_pmc(args.pmc, n)
+    unit_hash = _lib.build_info().get(HEADLINE_UNIT)
+    traffic, traffic_src = pmc_traffic(args.pmc, n, unit_hash)
 
     extra = {}
-    if rank == 0 and ws == 1 and not args.no_extra:
-        extra = extras(packed, dev)
+    if not args.no_extra:
+        if ws == 1:
+            extra = extras(packed, dev)
+        else:
+            extra = sharded_extras(packed, dev, rank, ws)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds)          # last: after every GPU leg
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": ws,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "gibson_multi_env_tau_grad (C3/C4 shape: %d pairs/GPU, %d "
                                    "envs, per-pair env id, dim 3)" % (n, args.envs),
                        "pairs_per_gpu": n, "global_batch": n_total, "envs": args.envs,
                        "grad_mode": args.mode, "allgather_outputs": gather,
-                       "parallelism": "dp%d" % ws},
+                       "parallelism": "dp%d" % ws,
+                       "rccl_world_size": tdist.get_world_size() if ws > 1 else 1},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": traffic, "kernel": "field_kernel<3,K_TAU_GRAD>",
-                         "kernel_ms": kern_ms, "flop_per_pair": FLOP_PER_PAIR,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "field_kernel<3,K_TAU_GRAD>", "unit_hash": unit_hash,
+                         "kernel_ms": kern_ms, "kernel_ms_min": float(kms.min()),
+                         "kernel_ms_max": float(kms.max()), "launches_timed": R,
+                         "flop_per_pair": FLOP_PER_PAIR,
                          "algorithmic_bytes_per_pair": BYTES_PER_PAIR},
             "cpu_baseline": cpu,
         }
@@ -165,24 +279,48 @@ def main():
     if ws > 1:
         tdist.barrier()
         tdist.destroy_process_group()
+    return 0
+
+
+def _timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def sharded_extras(packed, dev, rank, ws, q=1024):
+    """N > 1: the C5 arm planner with its 1024 queries sharded over the ranks, then the RCCL
+    all-gather of every rank's paths (the planner-path exchange of SURVEY.md §8e)."""
+    from pntf import ops, synth
+    Ba = torch.from_numpy(synth.make_B(6, seed=12, arm=True).T.copy()).to(dev)
+    xq_all = synth.make_box_pairs(q, 6, seed=3)
+    lo, hi = dist.shard_range(q, rank, ws)
+    xq = torch.from_numpy(xq_all[lo:hi].copy()).to(dev)
+    res = {}
+
+    def run():
+        path, steps = ops.plan(packed, xq, Ba, dim=6, step=0.015, tol=0.03, max_iter=199,
+                               mode=ops.GRAD_EXACT)
+        res["paths"] = dist.all_gather_rows(path, q)
+        res["steps"] = dist.all_gather_rows(steps, q)
+
+    el = timed(run, 3, 1, ws, torch.cuda.synchronize, dev)
+    return {"c5_arm_plan_1024q_sharded_allgather_ms": el / 3 * 1e3,
+            "c5_arm_plan_mean_steps": float(res["steps"].float().mean().item())}
 
 
 def extras(packed, dev):
     """Secondary configs measured after the headline (not part of `value`)."""
+    from pntf import ops, synth
     out = {}
-
-    def timeit(fn, reps=5):
-        fn()
-        torch.cuda.synchronize()
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(reps):
-            fn()
-        b.record()
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / reps
-
+    timeit = _timeit
     # C2: 262 144 pairs, single env
     n2 = 262144
     xp = torch.from_numpy(synth.make_pairs(n2, 3, seed=2)).to(dev)
@@ -196,10 +334,8 @@ def extras(packed, dev):
     # C1 shape on the GPU (4096 pairs, latency-bound): split tiles vs one wave per tile
     x1 = torch.from_numpy(synth.make_pairs(4096, 3, seed=2)).to(dev)
     for sched in ("auto", "wave_tile"):
-        ops.set_field_schedule(sched)
         out["c1_tau_grad_4096_us_" + sched] = 1e3 * timeit(
-            lambda: ops.tau_grad(packed, x1, B, dim=3), reps=20)
-    ops.set_field_schedule("auto")
+            lambda: ops.tau_grad(packed, x1, B, dim=3, schedule=sched), reps=20)
     # C3: Eikonal residual (Taylor mode + Model.Loss residual), 10 envs
     n3 = 1 << 20
     x3 = torch.from_numpy(synth.make_pairs(n3, 3, seed=5)).to(dev)
@@ -244,20 +380,12 @@ def mesh_extras(dev, n=1 << 20, t=20000, reps=3):
     """Speed-sample generator distance query (dataprocessing/speed_sampling_gpu.py:325-336):
     n sampled points against a t-triangle synthetic obstacle mesh (Gibson meshes are
     10^3..10^5 triangles).  VALU-bound; reported as point-triangle tests per second."""
+    from pntf import ops
     g = torch.Generator(device="cpu").manual_seed(9)
     tris = ((torch.rand(t, 1, 3, generator=g) - 0.5) * 0.8
             + torch.randn(t, 3, 3, generator=g) * 0.02).to(dev)
     pts = (torch.rand(n, 3, generator=g) - 0.5).to(dev)
-    ops.point_mesh_distance(pts, tris)
-    torch.cuda.synchronize()
-    a = torch.cuda.Event(enable_timing=True)
-    b = torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
-        ops.point_mesh_distance(pts, tris)
-    b.record()
-    torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / reps
+    ms = _timeit(lambda: ops.point_mesh_distance(pts, tris), reps=reps)
     return {"mesh_distance_1M_pts_20k_tris_ms": ms,
             "mesh_distance_point_tri_tests_per_s": n * t / (ms * 1e-3)}
 
@@ -270,6 +398,7 @@ def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=5):
     Loss forward + loss.backward() + AdamW step.  (2, 10000) is the reference's batch
     (Batch Size 2 environments x inner_batch 10000 pairs, :1010-1036)."""
     from models import model_res_sigmoid_multi as md
+    from pntf import synth
     from pntf.train import AdamW
     out = {}
     W = synth.make_weights(0)
@@ -303,13 +432,23 @@ def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=5):
     return out
 
 
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    if argv and argv[0] in ("--train-only", "--mesh-only"):
+        torch.cuda.set_device(0)
+        fn = train_extras if argv[0] == "--train-only" else mesh_extras
+        print(json.dumps(fn(torch.device("cuda", 0))), flush=True)
+        return 0
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one fresh process per GPU; this parent never initialises HIP
+        return launch.spawn(args.gpus, [os.path.abspath(__file__)] + list(argv))
+    ws = int(os.environ.get("WORLD_SIZE", 1))
+    if ws != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, ws), file=sys.stderr)
+        return 2
+    return rehearse(args) if args.rehearse else run(args)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "--train-only":
-        torch.cuda.set_device(0)
-        print(json.dumps(train_extras(torch.device("cuda", 0))), flush=True)
-        sys.exit(0)
-    if len(sys.argv) > 1 and sys.argv[1] == "--mesh-only":
-        torch.cuda.set_device(0)
-        print(json.dumps(mesh_extras(torch.device("cuda", 0))), flush=True)
-        sys.exit(0)
-    main()
+    sys.exit(main())

@@ -63,10 +63,16 @@ size_t pntf_packed_floats(void);
 int pntf_pack_weights(const float* const* params, int n_params, float* packed,
                       hipStream_t stream);
 
-/* Kernel schedule of pntf_tau / _tau_grad / _path_velocity / _speed / _travel_time
- * (PNTF_SCHED_*, see pntf_plan_ex; AUTO by default).  Process-wide setting: not thread-safe
- * against concurrent calls.  Results agree between schedules to fp32 rounding. */
+/* DEFAULT kernel schedule of pntf_tau / _tau_grad / _path_velocity / _speed / _travel_time
+ * (PNTF_SCHED_*, see pntf_plan_ex; AUTO unless changed).  Process-wide, so not thread-safe
+ * against concurrent calls: callers that need a specific schedule pass it per call through
+ * pntf_field_ex instead.  Results agree between schedules to fp32 rounding. */
 int pntf_set_field_schedule(int schedule);
+
+/* Build identity: "unit=hash;..." — one sha256 prefix per kernel translation unit (its
+ * source, the shared headers, defines and flags; p-ntfields_amd/pntf/build.py:unit_ids).
+ * Profiles under profiles/ record the hash of the unit they measured. */
+const char* pntf_build_info(void);
 
 /* Device scratch needed by the gradient/planner entry points for n pairs. */
 size_t pntf_workspace_bytes(int64_t n);
@@ -97,6 +103,19 @@ int pntf_speed(const float* packed, int dim, const float* xp, int64_t n, const f
 int pntf_travel_time(const float* packed, int dim, const float* xp, int64_t n,
                      const float* Btab, const int32_t* env, int32_t n_env, float* tt,
                      hipStream_t stream);
+
+/* Field kinds of pntf_field_ex (the entry points above, in this order). */
+#define PNTF_FIELD_TAU 0          /* pntf_tau:           out0 = tau (n)                     */
+#define PNTF_FIELD_TAU_GRAD 1     /* pntf_tau_grad:      out0 = tau (n), out1 = dtau        */
+#define PNTF_FIELD_VELOCITY 2     /* pntf_path_velocity: out0 = vel, out1 = tau (optional)  */
+#define PNTF_FIELD_SPEED 3        /* pntf_speed:         out0 = speed (n)                   */
+#define PNTF_FIELD_TRAVEL 4       /* pntf_travel_time:   out0 = tt (n)                      */
+
+/* Any of the five field entry points above with an explicit per-call schedule
+ * (PNTF_SCHED_*); `mode` is ignored by TAU/SPEED/TRAVEL, `ws` by TAU/TRAVEL. */
+int pntf_field_ex(int kind, const float* packed, int dim, const float* xp, int64_t n,
+                  const float* Btab, const int32_t* env, int32_t n_env, int mode, float* out0,
+                  float* out1, void* ws, size_t ws_bytes, int schedule, hipStream_t stream);
 
 /* Batched bidirectional planner = q independent copies of test/gib_plan.py:74-86
  * (Gibson: step 0.03, tol 0.06, max_iter 500, mode BACKGRAD_COMPAT) or

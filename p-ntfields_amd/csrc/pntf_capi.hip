@@ -87,8 +87,17 @@ static bool use_split(int64_t n, int schedule) {
   return (n + TILE - 1) / TILE <= 2 * (int64_t)num_cus();
 }
 
-// Schedule of the field entry points (pntf_set_field_schedule); process-wide.
+// Default schedule of the field entry points without an explicit one
+// (pntf_set_field_schedule); pntf_field_ex takes the schedule per call instead.
 static int g_field_schedule = PNTF_SCHED_AUTO;
+
+static bool valid_schedule(int s) {
+  return s == PNTF_SCHED_AUTO || s == PNTF_SCHED_WAVE_TILE || s == PNTF_SCHED_SPLIT_TILE;
+}
+
+#ifndef PNTF_BUILD_INFO
+#define PNTF_BUILD_INFO "unstamped"
+#endif
 
 // An empty batch is valid whatever the data pointers are (torch hands out NULL for empty
 // tensors); callers return PNTF_OK right after this check when n == 0.
@@ -131,15 +140,18 @@ static void launch_field(int kind, int64_t grid, const FieldArgs& a, hipStream_t
 
 static int run_field(int kind, const float* packed, int dim, const float* xp, int64_t n,
                      const float* Btab, const int32_t* env, int32_t n_env, int mode,
-                     float* out0, float* out1, void* ws, size_t ws_bytes, hipStream_t s) {
+                     float* out0, float* out1, void* ws, size_t ws_bytes, int schedule,
+                     hipStream_t s) {
   int st = check_common(packed, dim, xp, n, Btab, n_env);
   if (st) return st;
+  if (kind < K_TAU || kind > K_TRAVEL) return fail(PNTF_ERR_ARG, "unknown field kind%s");
+  if (!valid_schedule(schedule)) return fail(PNTF_ERR_ARG, "unknown schedule%s");
   if (mode != PNTF_GRAD_EXACT && mode != PNTF_GRAD_BACKGRAD_COMPAT)
     return fail(PNTF_ERR_ARG, "unknown gradient mode%s");
   if (n == 0) return PNTF_OK;
   if (!out0 || (kind == K_TAU_GRAD && !out1)) return fail(PNTF_ERR_ARG, "null output%s");
   const bool grad = kind != K_TAU && kind != K_TRAVEL;
-  const bool split = use_split(n, g_field_schedule);
+  const bool split = use_split(n, schedule);
   int64_t grid = split ? split_grid_for(n) : grid_for(n);
   if (grad) {
     if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
@@ -170,10 +182,10 @@ const char* pntf_last_error(void) { return g_err; }
 
 size_t pntf_packed_floats(void) { return (size_t)PACKED_FLOATS; }
 
+const char* pntf_build_info(void) { return PNTF_BUILD_INFO; }
+
 int pntf_set_field_schedule(int schedule) {
-  if (schedule != PNTF_SCHED_AUTO && schedule != PNTF_SCHED_WAVE_TILE &&
-      schedule != PNTF_SCHED_SPLIT_TILE)
-    return fail(PNTF_ERR_ARG, "unknown schedule%s");
+  if (!valid_schedule(schedule)) return fail(PNTF_ERR_ARG, "unknown schedule%s");
   g_field_schedule = schedule;
   return PNTF_OK;
 }
@@ -234,14 +246,14 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
 int pntf_tau(const float* packed, int dim, const float* xp, int64_t n, const float* Btab,
              const int32_t* env, int32_t n_env, float* tau, hipStream_t stream) {
   return run_field(K_TAU, packed, dim, xp, n, Btab, env, n_env, 0, tau, nullptr, nullptr, 0,
-                   stream);
+                   g_field_schedule, stream);
 }
 
 int pntf_tau_grad(const float* packed, int dim, const float* xp, int64_t n,
                   const float* Btab, const int32_t* env, int32_t n_env, int mode, float* tau,
                   float* dtau, void* ws, size_t ws_bytes, hipStream_t stream) {
   return run_field(K_TAU_GRAD, packed, dim, xp, n, Btab, env, n_env, mode, tau, dtau, ws,
-                   ws_bytes, stream);
+                   ws_bytes, g_field_schedule, stream);
 }
 
 int pntf_path_velocity(const float* packed, int dim, const float* xp, int64_t n,
@@ -249,21 +261,28 @@ int pntf_path_velocity(const float* packed, int dim, const float* xp, int64_t n,
                        float* vel, float* tau, void* ws, size_t ws_bytes,
                        hipStream_t stream) {
   return run_field(K_VELOCITY, packed, dim, xp, n, Btab, env, n_env, mode, vel, tau, ws,
-                   ws_bytes, stream);
+                   ws_bytes, g_field_schedule, stream);
 }
 
 int pntf_speed(const float* packed, int dim, const float* xp, int64_t n, const float* Btab,
                const int32_t* env, int32_t n_env, float* speed, void* ws, size_t ws_bytes,
                hipStream_t stream) {
   return run_field(K_SPEED, packed, dim, xp, n, Btab, env, n_env, PNTF_GRAD_EXACT, speed,
-                   nullptr, ws, ws_bytes, stream);
+                   nullptr, ws, ws_bytes, g_field_schedule, stream);
 }
 
 int pntf_travel_time(const float* packed, int dim, const float* xp, int64_t n,
                      const float* Btab, const int32_t* env, int32_t n_env, float* tt,
                      hipStream_t stream) {
   return run_field(K_TRAVEL, packed, dim, xp, n, Btab, env, n_env, 0, tt, nullptr, nullptr, 0,
-                   stream);
+                   g_field_schedule, stream);
+}
+
+int pntf_field_ex(int kind, const float* packed, int dim, const float* xp, int64_t n,
+                  const float* Btab, const int32_t* env, int32_t n_env, int mode, float* out0,
+                  float* out1, void* ws, size_t ws_bytes, int schedule, hipStream_t stream) {
+  return run_field(kind, packed, dim, xp, n, Btab, env, n_env, mode, out0, out1, ws, ws_bytes,
+                   schedule, stream);
 }
 
 int pntf_plan(const float* packed, int dim, const float* xp0, int64_t q, const float* Btab,
@@ -283,9 +302,7 @@ int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, cons
   if (max_iter < 0) return fail(PNTF_ERR_ARG, "max_iter must be >= 0%s");
   if (mode != PNTF_GRAD_EXACT && mode != PNTF_GRAD_BACKGRAD_COMPAT)
     return fail(PNTF_ERR_ARG, "unknown gradient mode%s");
-  if (schedule != PNTF_SCHED_AUTO && schedule != PNTF_SCHED_WAVE_TILE &&
-      schedule != PNTF_SCHED_SPLIT_TILE)
-    return fail(PNTF_ERR_ARG, "unknown schedule%s");
+  if (!valid_schedule(schedule)) return fail(PNTF_ERR_ARG, "unknown schedule%s");
   if (q == 0) return PNTF_OK;
   if (!path || !steps) return fail(PNTF_ERR_ARG, "null output%s");
   if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");

@@ -183,6 +183,8 @@ __global__ __launch_bounds__(BLOCK) void mesh_distance_kernel(
                     fmaxf(s_red[2][3 + d], s_red[3][3 + d]));
     }
   }
+  float pext = 0.f;  // largest |coordinate| of the workgroup's point box
+  for (int d = 0; d < 3; ++d) pext = fmaxf(pext, fmaxf(fabsf(lo[d]), fabsf(hi[d])));
   const int64_t t0 = (int64_t)blockIdx.y * per;
   const int64_t t1 = t0 + per < t ? t0 + per : t;
   for (int64_t base = t0; base < t1; base += BLOCK) {
@@ -202,7 +204,15 @@ __global__ __launch_bounds__(BLOCK) void mesh_distance_kernel(
       const float gx = fmaxf(fmaxf(bmin.x - hi[0], lo[0] - bmax.x), 0.f);
       const float gy = fmaxf(fmaxf(bmin.y - hi[1], lo[1] - bmax.y), 0.f);
       const float gz = fmaxf(fmaxf(bmin.z - hi[2], lo[2] - bmax.z), 0.f);
-      if (dot3(gx, gy, gz, gx, gy, gz) > bound) continue;
+      // Cull only with slack: gap^2 and tri_d2 are both fp32-rounded, and a triangle whose
+      // true distance sits within a few ulp of the box gap (axis-aligned walls) could
+      // otherwise be culled although its computed d2 is below the current best.  The slack
+      // covers both roundings: relative to the bound, and absolute on the squared
+      // coordinate scale of the triangle and the point box.
+      const float ext = fmaxf(fmaxf(fmaxf(fabsf(bmin.x), fabsf(bmax.x)),
+                                    fmaxf(fmaxf(fabsf(bmin.y), fabsf(bmax.y)),
+                                          fmaxf(fabsf(bmin.z), fabsf(bmax.z)))), pext);
+      if (dot3(gx, gy, gz, gx, gy, gz) > bound * (1.f + 1e-4f) + 1e-6f * ext * ext) continue;
 #pragma unroll
       for (int k = 0; k < PTS; ++k)
         best[k] = fminf(best[k], tri_d2(px[k], py[k], pz[k], s_rec + REC * j));

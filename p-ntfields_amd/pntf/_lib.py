@@ -29,6 +29,10 @@ SIGNATURES = {
                                          _c_void_p]),
     "pntf_workspace_bytes": (_size, [_i64]),
     "pntf_set_field_schedule": (ctypes.c_int, [ctypes.c_int]),
+    "pntf_build_info": (ctypes.c_char_p, []),
+    "pntf_field_ex": (ctypes.c_int, [ctypes.c_int, _c_void_p, ctypes.c_int, _c_void_p, _i64,
+                                     _c_void_p, _c_void_p, _i32, ctypes.c_int, _c_void_p,
+                                     _c_void_p, _c_void_p, _size, ctypes.c_int, _c_void_p]),
     "pntf_tau": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p, _c_void_p,
                                 _i32, _c_void_p, _c_void_p]),
     "pntf_tau_grad": (ctypes.c_int, [_c_void_p, ctypes.c_int, _c_void_p, _i64, _c_void_p,
@@ -103,6 +107,12 @@ def load():
         raise PntfError("libpntf ABI version mismatch")
     _lib = lib
     return lib
+
+
+def build_info():
+    """{unit: code hash} baked into the loaded libpntf.so (include/pntf.h pntf_build_info)."""
+    raw = load().pntf_build_info().decode()
+    return dict(kv.split("=", 1) for kv in raw.split(";") if "=" in kv)
 
 
 def check(status, what):

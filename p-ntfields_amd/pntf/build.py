@@ -77,6 +77,26 @@ def _stamp():
     return h.hexdigest()
 
 
+def unit_ids():
+    """Per-unit code identity: sha256 of the shared headers, the unit's source file, its
+    defines and the flags.  Baked into libpntf.so (pntf_build_info) so a PMC summary collected
+    from one build can be matched to the kernel that a later run actually loads."""
+    hdr = hashlib.sha256()
+    for name in sorted(os.listdir(CSRC)) + ["pntf.h"]:
+        if name.endswith(".h"):
+            path = os.path.join(INCLUDE if name == "pntf.h" else CSRC, name)
+            with open(path, "rb") as fh:
+                hdr.update(name.encode() + fh.read())
+    ids = {}
+    for name, src, defs in UNITS:
+        h = hdr.copy()
+        with open(os.path.join(CSRC, src), "rb") as fh:
+            h.update(fh.read())
+        h.update(repr((CXXFLAGS, defs)).encode())
+        ids[name] = h.hexdigest()[:16]
+    return ids
+
+
 def _resources(stderr):
     """Per-kernel register / spill figures from -Rpass-analysis=kernel-resource-usage."""
     out, cur = {}, None
@@ -97,6 +117,9 @@ def _compile(unit):
     d = os.path.join(BUILD, name)
     os.makedirs(d, exist_ok=True)
     obj = os.path.join(d, name + ".o")
+    if name == "capi":
+        defs = defs + ['-DPNTF_BUILD_INFO="%s"' % ";".join(
+            "%s=%s" % kv for kv in sorted(unit_ids().items()))]
     cmd = [hipcc()] + CXXFLAGS + defs + ["-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True, cwd=d)
     if r.returncode != 0:

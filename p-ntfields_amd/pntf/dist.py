@@ -19,14 +19,24 @@ def world():
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
-def init(backend=None):
-    """Initialise the default process group when launched with WORLD_SIZE > 1."""
+def init(backend=None, device=None):
+    """Initialise the default process group when launched with WORLD_SIZE > 1.
+
+    backend "nccl" is RCCL on ROCm (over xGMI inside a node); pass the rank's HIP `device`
+    (already made current) so the communicator binds to it.  Returns (rank, world_size) as
+    the process group reports them, which must equal the environment's."""
     rank, ws, _ = world()
     if ws > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend=backend, rank=rank, world_size=ws)
+        kw = {"device_id": device} if (device is not None and backend == "nccl") else {}
+        dist.init_process_group(backend=backend, rank=rank, world_size=ws, **kw)
+    if dist.is_initialized():
+        got = (dist.get_rank(), dist.get_world_size())
+        if got != (rank, ws):
+            raise RuntimeError("process group reports rank/world %s, environment %s"
+                               % (got, (rank, ws)))
     return rank, ws
 
 
@@ -45,6 +55,13 @@ def all_gather_rows(local, n_total, group=None):
     if ws == 1:
         return local
     chunk = -(-n_total // ws)
+    if n_total == chunk * ws:                 # equal shards: gather straight into the result
+        if local.shape[0] != chunk:
+            raise ValueError("rank holds %d rows, expected %d" % (local.shape[0], chunk))
+        out = torch.empty((n_total,) + tuple(local.shape[1:]), dtype=local.dtype,
+                          device=local.device)
+        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+        return out
     pad = torch.zeros((chunk,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
     out = torch.empty((chunk * ws,) + tuple(local.shape[1:]), dtype=local.dtype,

@@ -3,6 +3,11 @@
 Every call is stream-ordered on torch's current HIP stream of the input's device; torch's
 caching allocator owns all buffers (outputs and the scratch workspace).  Inputs must be
 HIP (``cuda``) tensors: there is deliberately no CPU path.
+
+The scratch workspace is cached per (device, stream): two streams of one device never share
+a slot set, so concurrent calls on different streams cannot overwrite each other's saved σ
+tiles.  The kernel schedule is an argument of every call (pntf_field_ex); nothing here
+mutates process-wide library state.
 """
 import ctypes
 
@@ -41,12 +46,16 @@ def workspace_bytes(n):
 
 
 def _workspace(device, n):
-    """Grow-only scratch buffer per device (saved σ10 tiles of the reverse sweep)."""
+    """Grow-only scratch buffer per (device, stream) (saved σ10 tiles of the reverse sweep).
+    Memory is recorded on the stream it serves, so the caching allocator keeps it alive until
+    that stream's work is done even when a larger buffer replaces it."""
     need = workspace_bytes(n)
-    key = (device.type, device.index)
+    stream = torch.cuda.current_stream(device)
+    key = (device.index, stream.cuda_stream)
     ws = _ws_cache.get(key)
     if ws is None or ws.numel() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=device)
+        ws.record_stream(stream)
         _ws_cache[key] = ws
     return ws
 
@@ -92,78 +101,72 @@ def _prep(xp, Btab, env, dim):
     return xp, Bt, env
 
 
-def tau(packed, xp, Btab, env=None, dim=3):
-    """τ (n,) — NN.out (model_res_sigmoid_multi.py:215-259)."""
-    lib = _lib.load()
-    xp, Bt, env = _prep(xp, Btab, env, dim)
+SCHEDULES = {"auto": 0, "wave_tile": 1, "split_tile": 2}
+FIELD_TAU, FIELD_TAU_GRAD, FIELD_VELOCITY, FIELD_SPEED, FIELD_TRAVEL = range(5)
+
+
+def _sched(schedule):
+    if schedule not in SCHEDULES:
+        raise PntfError("unknown schedule %r (one of %s)" % (schedule, sorted(SCHEDULES)))
+    return SCHEDULES[schedule]
+
+
+def _field(kind, packed, xp, Bt, env, dim, mode, out0, out1, ws, schedule, what):
     n = xp.shape[0]
-    out = torch.empty(n, dtype=torch.float32, device=xp.device)
-    check(lib.pntf_tau(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0], _vp(out),
-                       _stream(xp.device)), "pntf_tau")
+    check(_lib.load().pntf_field_ex(kind, _vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env),
+                                    Bt.shape[0], mode, _vp(out0), _vp(out1), _vp(ws),
+                                    ws.numel() if ws is not None else 0, _sched(schedule),
+                                    _stream(xp.device)), what)
+
+
+def tau(packed, xp, Btab, env=None, dim=3, schedule="auto"):
+    """τ (n,) — NN.out (model_res_sigmoid_multi.py:215-259)."""
+    xp, Bt, env = _prep(xp, Btab, env, dim)
+    out = torch.empty(xp.shape[0], dtype=torch.float32, device=xp.device)
+    _field(FIELD_TAU, packed, xp, Bt, env, dim, 0, out, None, None, schedule, "pntf_tau")
     return out
 
 
-def tau_grad(packed, xp, Btab, env=None, dim=3, mode=GRAD_EXACT):
+def tau_grad(packed, xp, Btab, env=None, dim=3, mode=GRAD_EXACT, schedule="auto"):
     """τ (n,) and ∇τ (n, 2dim): Model.gradient(NN.out) (EXACT) or NN.out_backgrad (COMPAT)."""
-    lib = _lib.load()
     xp, Bt, env = _prep(xp, Btab, env, dim)
     n = xp.shape[0]
     t = torch.empty(n, dtype=torch.float32, device=xp.device)
     d = torch.empty((n, 2 * dim), dtype=torch.float32, device=xp.device)
-    ws = _workspace(xp.device, n)
-    check(lib.pntf_tau_grad(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0], mode,
-                            _vp(t), _vp(d), _vp(ws), ws.numel(), _stream(xp.device)),
-          "pntf_tau_grad")
+    _field(FIELD_TAU_GRAD, packed, xp, Bt, env, dim, mode, t, d, _workspace(xp.device, n),
+           schedule, "pntf_tau_grad")
     return t, d
 
 
-def path_velocity(packed, xp, Btab, env=None, dim=3, mode=GRAD_BACKGRAD_COMPAT):
+def path_velocity(packed, xp, Btab, env=None, dim=3, mode=GRAD_BACKGRAD_COMPAT,
+                  schedule="auto"):
     """[v_start | v_goal] (n, 2dim) and τ (n,) — Model.Gradient (:1218-1248)."""
-    lib = _lib.load()
     xp, Bt, env = _prep(xp, Btab, env, dim)
     n = xp.shape[0]
     v = torch.empty((n, 2 * dim), dtype=torch.float32, device=xp.device)
     t = torch.empty(n, dtype=torch.float32, device=xp.device)
-    ws = _workspace(xp.device, n)
-    check(lib.pntf_path_velocity(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0],
-                                 mode, _vp(v), _vp(t), _vp(ws), ws.numel(), _stream(xp.device)),
-          "pntf_path_velocity")
+    _field(FIELD_VELOCITY, packed, xp, Bt, env, dim, mode, v, t, _workspace(xp.device, n),
+           schedule, "pntf_path_velocity")
     return v, t
 
 
-def speed(packed, xp, Btab, env=None, dim=3):
+def speed(packed, xp, Btab, env=None, dim=3, schedule="auto"):
     """Speed at the goal (n,) — Model.Speed (:1195-1216)."""
-    lib = _lib.load()
     xp, Bt, env = _prep(xp, Btab, env, dim)
     n = xp.shape[0]
     s = torch.empty(n, dtype=torch.float32, device=xp.device)
-    ws = _workspace(xp.device, n)
-    check(lib.pntf_speed(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0], _vp(s),
-                         _vp(ws), ws.numel(), _stream(xp.device)), "pntf_speed")
+    _field(FIELD_SPEED, packed, xp, Bt, env, dim, GRAD_EXACT, s, None,
+           _workspace(xp.device, n), schedule, "pntf_speed")
     return s
 
 
-def travel_time(packed, xp, Btab, env=None, dim=3):
+def travel_time(packed, xp, Btab, env=None, dim=3, schedule="auto"):
     """|x_g - x_s| / τ (n,) — Model.TravelTimes (:1173-1186)."""
-    lib = _lib.load()
     xp, Bt, env = _prep(xp, Btab, env, dim)
-    n = xp.shape[0]
-    tt = torch.empty(n, dtype=torch.float32, device=xp.device)
-    check(lib.pntf_travel_time(_vp(packed), dim, _vp(xp), n, _vp(Bt), _vp(env), Bt.shape[0],
-                               _vp(tt), _stream(xp.device)), "pntf_travel_time")
+    tt = torch.empty(xp.shape[0], dtype=torch.float32, device=xp.device)
+    _field(FIELD_TRAVEL, packed, xp, Bt, env, dim, 0, tt, None, None, schedule,
+           "pntf_travel_time")
     return tt
-
-
-SCHEDULES = {"auto": 0, "wave_tile": 1, "split_tile": 2}
-
-
-def set_field_schedule(schedule):
-    """Kernel schedule of tau / tau_grad / path_velocity / speed / travel_time
-    (include/pntf.h pntf_set_field_schedule): "auto" (default: split tiles for batches of at
-    most 2 x CUs x 16 pairs), "wave_tile" or "split_tile".  Process-wide."""
-    if schedule not in SCHEDULES:
-        raise PntfError("unknown schedule %r" % (schedule,))
-    check(_lib.load().pntf_set_field_schedule(SCHEDULES[schedule]), "pntf_set_field_schedule")
 
 
 def plan(packed, xp0, Btab, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
@@ -174,8 +177,7 @@ def plan(packed, xp0, Btab, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
     state — and steps (q,) int32 (updates taken per query).  `schedule` picks the kernel
     (include/pntf.h pntf_plan_ex): "wave_tile" (one wave per 16 queries), "split_tile" (four
     waves share 16 queries: lower latency per step) or "auto"."""
-    if schedule not in SCHEDULES:
-        raise PntfError("unknown schedule %r" % (schedule,))
+    sched = _sched(schedule)
     lib = _lib.load()
     xp0, Bt, env = _prep(xp0, Btab, env, dim)
     q = xp0.shape[0]
@@ -184,7 +186,7 @@ def plan(packed, xp0, Btab, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
     ws = _workspace(xp0.device, q)
     check(lib.pntf_plan_ex(_vp(packed), dim, _vp(xp0), q, _vp(Bt), _vp(env), Bt.shape[0],
                            mode, float(step), float(tol), int(max_iter), _vp(path), _vp(steps),
-                           _vp(ws), ws.numel(), SCHEDULES[schedule], _stream(xp0.device)),
+                           _vp(ws), ws.numel(), sched, _stream(xp0.device)),
           "pntf_plan_ex")
     return path, steps
 

@@ -52,11 +52,14 @@ _partial_cache = {}
 
 
 def _partial(device):
-    key = (device.type, device.index)
+    """Reduction scratch per (device, stream): calls on different streams never share it."""
+    stream = torch.cuda.current_stream(device)
+    key = (device.index, stream.cuda_stream)
     buf = _partial_cache.get(key)
     if buf is None:
         buf = torch.empty(int(_lib.load().pntf_tt_partial_floats()), dtype=torch.float32,
                           device=device)
+        buf.record_stream(stream)
         _partial_cache[key] = buf
     return buf
 

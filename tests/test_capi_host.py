@@ -146,3 +146,52 @@ def test_synth_is_deterministic():
     assert x.shape == (5000, 6) and np.all(np.abs(x) <= 0.5)
     e = synth.make_env_ids(1048576, 10)
     assert e.min() == 0 and e.max() == 9 and np.all(np.diff(e) >= 0)
+
+
+def test_field_ex_validates_kind_and_schedule_without_gpu():
+    L = _lib.load()
+    fake = ctypes.c_void_p(16)
+    assert L.pntf_field_ex(9, fake, 3, fake, 4, fake, None, 1, 0, fake, fake, fake, 1 << 30, 0,
+                           None) == 1
+    assert b"kind" in L.pntf_last_error()
+    assert L.pntf_field_ex(1, fake, 3, fake, 4, fake, None, 1, 0, fake, fake, fake, 1 << 30, 5,
+                           None) == 1
+    assert b"schedule" in L.pntf_last_error()
+    # empty batch: valid for every kind and schedule, nothing launched
+    for kind in range(5):
+        for sched in range(3):
+            assert L.pntf_field_ex(kind, None, 3, None, 0, None, None, 1, 0, None, None, None, 0,
+                                   sched, None) == 0
+
+
+def test_build_info_names_every_kernel_unit():
+    from pntf import build
+    info = _lib.build_info()
+    assert set(info) == {u[0] for u in build.UNITS}
+    assert info == build.unit_ids()          # the loaded library is the current source
+
+
+def _asm(unit):
+    from pntf import build
+    import glob
+    files = glob.glob(os.path.join(build.BUILD, unit, "*amdgcn*gfx950*.s"))
+    if not files:
+        pytest.skip("device assembly of %s not kept (build dir absent)" % unit)
+    return open(files[0]).read()
+
+
+@pytest.mark.parametrize("unit", ["field_d3_k1", "field_d6_k1", "plan_d6", "fsplit_d3_k1"])
+def test_scratch_reloads_bypass_l1(unit):
+    """Regression guard for DESIGN §7.3: a persistent wave rewrites its saved-σ slot for every
+    tile and its stores do not refresh the CU's L1, so every load through the scratch buffer
+    resource must carry the `nt` policy (a build without it returned stale σ tiles)."""
+    asm = _asm(unit)
+    op = r"\s+v\[?[\d:]+\]?,\s+v\d+,\s+(s\[\d+:\d+\]),"     # data, voffset, resource
+    stores = re.findall(r"buffer_store_dwordx4" + op, asm)
+    assert stores, "no scratch stores found"
+    assert all(" nt" in l for l in re.findall(r"buffer_store_dwordx4.*", asm))
+    res = set(stores)
+    loads = [l for l in re.findall(r"buffer_load_dwordx4" + op + "(.*)", asm) if l[0] in res]
+    assert len(loads) >= len(re.findall(r"buffer_store_dwordx4", asm))
+    bad = [l for l in loads if not l[1].rstrip().endswith(" nt")]
+    assert not bad, bad[:3]

@@ -3,27 +3,36 @@ the CPU oracle.
 
 Tolerance (BASELINE.json north_star): τ and ∇τ within 1e-4 relative (fp32) of the
 reference — checked as relative L2 over the batch AND as the max abs error over the max
-|value|; planner endpoints within 1e-3 of the reference's batch-1 loop.
+|value| — and, elementwise, every value within ELEM relative of the reference's, with
+relative error measured against max(|ref|, ELEM_FLOOR · max|ref|): a component of ∇τ that is
+off by 10 % or more fails unless it is below 1e-3 of the batch's largest component (where the
+fp32 reference itself carries ~1e-4 relative noise: oracle fp64 vs reference 1.4e-4).
+Planner endpoints within 1e-3 of the reference's batch-1 loop.
 """
 import numpy as np
 import pytest
 import torch
 
-from golden_util import load, rel_l2, weights
+from golden_util import load, max_rel, rel_l2, weights
 from oracle import pntf_oracle as O
 from pntf import ops, synth
 
 pytestmark = pytest.mark.gpu
 
 REL = 1e-4
+ELEM = 1e-3
+ELEM_FLOOR = 1e-2
 
 
-def close(a, b, tol=REL):
+def close(a, b, tol=REL, elem=ELEM):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     l2 = rel_l2(a, b)
-    mx = float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
-    assert l2 < tol and mx < tol, "rel_l2=%.3g max=%.3g (tol %.1g)" % (l2, mx, tol)
+    scale = max(np.abs(b).max(), 1e-30)
+    mx = float(np.abs(a - b).max() / scale)
+    el = max_rel(a, b, ELEM_FLOOR * scale)
+    assert l2 < tol and mx < tol and el < elem, \
+        "rel_l2=%.3g max=%.3g elementwise=%.3g (tol %.1g, elem %.1g)" % (l2, mx, el, tol, elem)
 
 
 @pytest.fixture(scope="module")
@@ -44,10 +53,9 @@ def packed(W, dev):
 
 @pytest.fixture(params=["wave_tile", "split_tile"])
 def field_schedule(request):
-    """Run a field test with one wave per tile and with split tiles (pntf_split.h)."""
-    ops.set_field_schedule(request.param)
-    yield request.param
-    ops.set_field_schedule("auto")
+    """Run a field test with one wave per tile and with split tiles (pntf_split.h); the
+    schedule is passed per call (pntf_field_ex), no library state changes."""
+    return request.param
 
 
 def T(a, dev, dtype=torch.float32):
@@ -56,7 +64,7 @@ def T(a, dev, dtype=torch.float32):
 
 def test_tau_grad_exact_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
-    t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3, mode=ops.GRAD_EXACT)
+    t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3, mode=ops.GRAD_EXACT, schedule=field_schedule)
     close(t.cpu().numpy(), f["tau"][:, 0])
     close(d.cpu().numpy(), f["dtau"])
     close(d.cpu().numpy(), f["dtau_fwdmode"])
@@ -64,14 +72,14 @@ def test_tau_grad_exact_vs_reference(packed, dev, field_schedule):
 
 def test_tau_only_kernel(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
-    t = ops.tau(packed, T(f["xp"], dev), T(f["B"], dev), dim=3)
+    t = ops.tau(packed, T(f["xp"], dev), T(f["B"], dev), dim=3, schedule=field_schedule)
     close(t.cpu().numpy(), f["tau"][:, 0])
 
 
 def test_backgrad_compat_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3,
-                        mode=ops.GRAD_BACKGRAD_COMPAT)
+                        mode=ops.GRAD_BACKGRAD_COMPAT, schedule=field_schedule)
     close(t.cpu().numpy(), f["tau_backgrad"][:, 0])
     close(d.cpu().numpy(), f["dtau_backgrad"])
 
@@ -79,29 +87,29 @@ def test_backgrad_compat_vs_reference(packed, dev, field_schedule):
 def test_epilogues_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     xp, B = T(f["xp"], dev), T(f["B"], dev)
-    v, _ = ops.path_velocity(packed, xp, B, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT)
+    v, _ = ops.path_velocity(packed, xp, B, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT, schedule=field_schedule)
     close(v.cpu().numpy(), f["gradient"])
-    close(ops.speed(packed, xp, B, dim=3).cpu().numpy(), f["speed"])
-    close(ops.travel_time(packed, xp, B, dim=3).cpu().numpy(), f["travel_time"])
+    close(ops.speed(packed, xp, B, dim=3, schedule=field_schedule).cpu().numpy(), f["speed"])
+    close(ops.travel_time(packed, xp, B, dim=3, schedule=field_schedule).cpu().numpy(), f["travel_time"])
 
 
 def test_env_table_vs_reference(packed, dev, field_schedule):
     g = load("fwd_grad_env_d3.npz")
     xp, Bt, env = T(g["xp"], dev), T(g["B_table"], dev), T(g["env"], dev, torch.int32)
-    t, d = ops.tau_grad(packed, xp, Bt, env, dim=3)
+    t, d = ops.tau_grad(packed, xp, Bt, env, dim=3, schedule=field_schedule)
     close(t.cpu().numpy(), g["tau"][:, 0])
     close(d.cpu().numpy(), g["dtau"])
-    _, dc = ops.tau_grad(packed, xp, Bt, env, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT)
+    _, dc = ops.tau_grad(packed, xp, Bt, env, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT, schedule=field_schedule)
     close(dc.cpu().numpy(), g["dtau_backgrad"])
 
 
 def test_arm_dim6_vs_reference(packed, dev, field_schedule):
     a = load("fwd_grad_d6.npz")
     xp, B = T(a["xp"], dev), T(a["B"].T, dev)
-    t, d = ops.tau_grad(packed, xp, B, dim=6)
+    t, d = ops.tau_grad(packed, xp, B, dim=6, schedule=field_schedule)
     close(t.cpu().numpy(), a["tau"][:, 0])
     close(d.cpu().numpy(), a["dtau"])
-    v, _ = ops.path_velocity(packed, xp[:16], B, dim=6, mode=ops.GRAD_EXACT)
+    v, _ = ops.path_velocity(packed, xp[:16], B, dim=6, mode=ops.GRAD_EXACT, schedule=field_schedule)
     close(v.cpu().numpy(), a["gradient16"])
 
 
@@ -110,7 +118,7 @@ def test_ragged_batches_vs_oracle(packed, dev, W, field_schedule, n):
     xp = synth.make_pairs(n, 3, seed=100 + n)
     Bt = synth.make_B_table(3, 3, first_seed=20)
     env = synth.make_env_ids(n, 3, contiguous=False, seed=n)
-    t, d = ops.tau_grad(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3)
+    t, d = ops.tau_grad(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3, schedule=field_schedule)
     to, do = O.tau_grad(W, xp, Bt, env)
     close(t.cpu().numpy(), to[:, 0])
     close(d.cpu().numpy(), do)
@@ -128,7 +136,7 @@ def test_invalid_env_gives_nan(packed, dev, field_schedule):
     env = np.zeros(20, np.int32)
     env[3] = 7
     env[11] = -1
-    t, d = ops.tau_grad(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3)
+    t, d = ops.tau_grad(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3, schedule=field_schedule)
     t, d = t.cpu().numpy(), d.cpu().numpy()
     assert np.isnan(t[3]) and np.isnan(t[11]) and np.isnan(d[3]).all()
     ok = np.ones(20, bool)

@@ -117,6 +117,19 @@ def test_hip_distance_bits_independent_of_triangle_split():
             for o in (False, True)]
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
+    # axis-aligned walls (Gibson-like rooms): many triangles whose true distance equals the
+    # culling box gap to the last ulp; points on a lattice aligned with the walls
+    walls = np.concatenate([M.box_mesh(np.array([-0.4, -0.3, -0.25]) + 0.1 * k,
+                                       np.array([-0.2, 0.1, 0.05]) + 0.1 * k)
+                            for k in range(6)]).astype(np.float32)
+    g = np.linspace(-0.5, 0.5, 41, dtype=np.float32)
+    lat = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)
+    W, P = torch.from_numpy(walls).cuda(), torch.from_numpy(lat).cuda()
+    ref = ops.point_mesh_distance(P, W, chunks=1, order=False)
+    for c in (1, 3, 0):
+        assert torch.equal(ops.point_mesh_distance(P, W, chunks=c, order=True), ref)
+    sub = rng.choice(lat.shape[0], 1500, replace=False)
+    assert np.abs(ref.cpu().numpy()[sub] - M.point_mesh_distance(lat[sub], walls)).max() < TOL
 
 
 @pytest.mark.gpu

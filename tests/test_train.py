@@ -127,18 +127,36 @@ def test_two_adamw_steps_vs_reference(name, dim):
     f = load(name)
     model, net = _nets(dim, W, dev, f["B"] if dim == 6 else None)
     opt = AdamW(net.parameters(), lr=1e-3, weight_decay=0.1)
+    grads = []
     for step in range(2):
         loss, loss_n, _ = _loss(model, f, dim, dev)
         if step == 1:
             assert abs(loss.item() - float(f["loss2"])) < 1e-5 * max(1.0, float(f["loss2"]))
         loss.backward()
+        grads.append({k: p.grad.detach().cpu().numpy().copy()
+                      for k, p in net.named_parameters() if p.grad is not None})
         opt.step()
         opt.zero_grad()
     sd = net.state_dict()
+    # An Adam update is lr * m/sqrt(v), so a gradient error δ moves it by ~lr * δ/|g|.  Each
+    # element is held to 2e-6 plus that propagated amount, with δ the gradient error actually
+    # measured against the reference's step-1 gradient: an element whose gradient is well
+    # resolved (|g| >> δ) must match to ~2e-6, while a sign or indexing bug (an error of
+    # ~lr = 1e-3 on a well-resolved element) fails.
+    lr = 1e-3
     for k in f.files:
         if k.startswith("after2:"):
-            err = np.abs(sd[k[7:]].cpu().numpy() - f[k])
-            assert np.mean(err < 1e-6) >= 0.99 and err.max() < 4e-3, (k, err.max())
+            name = k[7:]
+            got = sd[name].cpu().numpy()
+            if name not in grads[0]:                 # encoder1.0: no gradient, unchanged
+                assert np.array_equal(got, f[k]), name
+                continue
+            err = np.abs(got - f[k])
+            delta = max(float(np.abs(grads[0][name] - f["grad:" + name]).max()), 1e-12)
+            g = np.minimum(np.abs(grads[0][name]), np.abs(grads[1][name]))
+            bound = 2e-6 + 4 * lr * delta / np.maximum(g, delta)
+            worst = np.argmax(err - bound)
+            assert (err <= bound).all(), (name, float(err.flat[worst]), float(bound.flat[worst]))
     assert np.array_equal(sd["encoder1.0.weight"].cpu().numpy(), W["encoder1.0.weight"])
 
 

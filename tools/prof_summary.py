@@ -35,7 +35,12 @@ def main():
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--pairs", type=int, default=1 << 20)
     ap.add_argument("--kernel", default="field_kernel<3, 1>")
+    ap.add_argument("--unit", default="field_d3_k1", help="build unit of --kernel")
     a = ap.parse_args()
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "p-ntfields_amd"))
+    from pntf import _lib
+    unit_hash = _lib.build_info()[a.unit]      # the library these profiles were taken from
     os.makedirs(PROF, exist_ok=True)
     stats = os.path.join(OUT, "prof_stats", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(PROF, "%s_kernel_stats.csv" % a.tag))
@@ -52,7 +57,8 @@ def main():
     clock = mfma["GRBM_GUI_ACTIVE"] / 8 / (avg_ns * 1e-9) / 1e9
     simd_cycles = 1024 * avg_ns * 1e-9 * clock * 1e9
     j = {
-        "kernel": a.kernel, "pairs_per_launch": a.pairs, "avg_duration_ns": avg_ns,
+        "kernel": a.kernel, "unit": a.unit, "unit_hash": unit_hash,
+        "pairs_per_launch": a.pairs, "avg_duration_ns": avg_ns,
         "FETCH_SIZE_KiB": fetch["FETCH_SIZE"], "WRITE_SIZE_KiB": write["WRITE_SIZE"],
         "fetch_bytes_corrected_x2": fetch_b, "write_bytes": write_b,
         "hbm_bytes_per_launch": fetch_b + write_b,

@@ -8,7 +8,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --no-cpu --no-extra"
+BENCH="$R/bench.py --no-cpu --no-extra --roofline-launches 1"
 run() {  # run <dir> <seconds> <rocprofv3 args...>
   local d=$1 t=$2; shift 2
   timeout -k 10 "$t" rocprofv3 "$@" -d "$OUT/$d" -o run --output-format csv -- \

@@ -50,7 +50,7 @@ HEADLINE_UNIT = "field_d3_k1"      # build unit of field_kernel<3, K_TAU_GRAD> (
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pairs", type=int, default=1 << 20, help="pairs per GPU (weak scaling)")
     ap.add_argument("--total-pairs", type=int, default=0,

@@ -128,6 +128,16 @@ def forward(params, xp, B, env=None, dim=3, dtype=np.float64, keep=False):
     return tau, dict(p=p, q=q, w=w, per=per, enc=enc, s0=s0, gen=gen, n=n, dim=dim)
 
 
+def softplus_saturation(params, xp, B, dim=3):
+    """Fraction of all softplus pre-activations (encoder, generator, generator[3]) that take
+    torch Softplus's identity branch (10y > 20) — how much of that branch a fixture covers."""
+    _, st = forward(params, xp, B, dim=dim, keep=True)
+    ys = [st["enc"]["e0"], st["gen"]["g3"]]
+    for blk in st["enc"]["blk"] + st["gen"]["blk"]:
+        ys += list(blk)
+    return sum(float((SCALE * y > THRESH).sum()) for y in ys) / sum(y.size for y in ys)
+
+
 # ------------------------------------------------------------------ reverse mode (A6/A7)
 
 

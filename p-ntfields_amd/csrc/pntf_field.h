@@ -103,6 +103,19 @@ __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 #ifndef PNTF_IGLP_V
 #define PNTF_IGLP_V 0
 #endif
+#ifndef PNTF_IGLP_CLUSTER
+#define PNTF_IGLP_CLUSTER 0
+#endif
+// Deferred epilogues after the step's MFMAs (1) or before them (0).  Before, the first unit
+// of a group reads accumulators whose last MFMA was issued in the step just before, so the
+// wave waits for that MFMA to drain (s_nop + dependency) with no MFMA of its own in flight.
+#ifndef PNTF_EPI_LATE
+#define PNTF_EPI_LATE 0
+#endif
+// Groups of lead for the saved-σ loads of the encoder's reverse layers (Bwd AH).
+#ifndef PNTF_ENC_AH
+#define PNTF_ENC_AH 1
+#endif
 // Packed weights are read through a buffer resource: per-lane voffset = lane*16 and a
 // scalar byte offset per fragment, so address math stays on the SALU.
 typedef __amdgpu_buffer_rsrc_t Rsrc;
@@ -180,6 +193,23 @@ __device__ __forceinline__ void run_steps(Ring& ring, Rsrc r, int voff, AddrF ad
         ring.r[slot][l] = bload(r, voff, naddr(S + PF_STEPS - STEPS, l));
     }
     body(st, a);
+#if PNTF_IGLP_CLUSTER == 1
+    // One VALU cluster per step: beside f32 MFMAs every gap that carries vector work pays a
+    // switch cost (tests/diag/coexec_probe.hip: ~12-17 cycles for the first VALU op in a
+    // gap, 4-8 for each further one), so the step's loads go first, then its MFMAs, then all
+    // its VALU work in one gap (data dependencies still order a pre hook's VALU before the
+    // MFMAs that read its results).
+    __builtin_amdgcn_sched_group_barrier(0x020, 16, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 512, 0);
+    __builtin_amdgcn_sched_group_barrier(0x040, 16, 0);
+#elif PNTF_IGLP_CLUSTER == 2
+    // VALU first, then loads and MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x002, 512, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 16, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);
+    __builtin_amdgcn_sched_group_barrier(0x040, 16, 0);
+#endif
 #if PNTF_IGLP_V > 0
     // Interleave the step as (1 MFMA, PNTF_IGLP_V VALU) x 16 so dependent VALU chains of the
     // deferred epilogues sit between MFMAs instead of stalling the wave's in-order issue.
@@ -230,7 +260,11 @@ __device__ __forceinline__ f32x4 ld4(const float* p) {
 // stores of tile k+1 do not refresh the CU's vector L1, and a plain load would hit the L1
 // lines of tile k (measured: ~3% stale ∇τ values at 262k pairs).  nt loads bypass L1
 // (MI355X_MICROARCH.md, inter-workgroup visibility table).
+#ifndef PNTF_SCRATCH_LOAD_AUX  // overridden only by the build-guard test (tests/test_capi_host.py)
+#define PNTF_SCRATCH_LOAD_AUX 2
+#endif
 constexpr int AUX_NT = 2;
+constexpr int AUX_LOAD = PNTF_SCRATCH_LOAD_AUX;
 struct Scratch {
   Rsrc r;
 };
@@ -251,7 +285,7 @@ __device__ __forceinline__ f32x4 load_tile(Scratch sc, int tile, int lane) {
   return f32x4{0.5f, 0.5f, 0.5f, 0.5f};
 #endif
   return __builtin_bit_cast(
-      f32x4, __builtin_amdgcn_raw_buffer_load_b128(sc.r, lane * 16, tile * 1024, AUX_NT));
+      f32x4, __builtin_amdgcn_raw_buffer_load_b128(sc.r, lane * 16, tile * 1024, AUX_LOAD));
 }
 // Between the forward sweep (stores) and the reverse sweep (loads of the same slot): wait
 // until every store of this wave has been performed.  Without it the first reverse-sweep
@@ -291,15 +325,23 @@ struct NoPre {
 #define PNTF_EP_SPLIT 2
 #endif
 constexpr int EP_SPLIT = PNTF_EP_SPLIT;
-constexpr int EP_ROWS = 4 / EP_SPLIT;
+// k tiles per step in the encoder layers (2: 16 MFMAs and 2 weight fragments per step; 4: 32
+// MFMAs and 4 fragments, so the 4-step ring runs twice as far ahead in time) and the
+// matching epilogue units per out tile.
+#ifndef PNTF_ENC_KS
+#define PNTF_ENC_KS 2
+#endif
+constexpr int EKS = PNTF_ENC_KS;
+constexpr int EEPS = EKS == 4 ? 1 : EP_SPLIT;
+constexpr int EGS = 8 / EKS;                 // steps per encoder group (1 out tile x 2 cols)
 
 // One Linear layer as out-tile groups of NO tiles x NC columns (NO*NC >= 2 independent MFMA
 // chains); a step consumes KS k-tiles (NO*KS weight fragments), KT/KS steps per group.  The
 // layer object ly supplies
 //   ly.init(ot, acc)      at the first step of the group starting at out tile ot
-//   ly.epi(t, c, h, v)    unit h (rows h*EP_ROWS ..) of the epilogue of out tile t, column c,
+//   ly.epi(t, c, h, v)    unit h (rows h*4/EPS ..) of the epilogue of out tile t, column c,
 //                         from v[NC] = that tile's accumulators; runs deferred, one unit per
-//                         step in the first NO*NC*EP_SPLIT steps of the next group
+//                         step in the first NO*NC*EPS steps of the next group
 //   ly.pend[NO][NC]       holds the last group's accumulators on return: its epilogue is
 //                         still pending (run it with flush(), or as the next layer's pre hook)
 // pre(st) runs at every step (the previous layer's pending tail; a no-op past its length).
@@ -311,7 +353,8 @@ __device__ __forceinline__ void layer(Ring& ring, Rsrc W, int wbase, const f32x4
   static_assert(L::OT == OT && L::NC == NC, "layer object shape");
   constexpr int GS = KT / KS;                 // steps per group
   constexpr int STEPS = (OT / NO) * GS;
-  constexpr int UNITS = NO * NC * EP_SPLIT;   // deferred epilogue units per group
+  constexpr int EPS = L::EPS;                 // epilogue units per out tile
+  constexpr int UNITS = NO * NC * EPS;        // deferred epilogue units per group
   static_assert(KT % KS == 0 && UNITS <= GS, "a group's epilogue must fit in the next group");
   f32x4 acc[NO][NC];
   run_steps<STEPS, NO * KS, NLN, SITE>(
@@ -325,11 +368,14 @@ __device__ __forceinline__ void layer(Ring& ring, Rsrc W, int wbase, const f32x4
         constexpr int ot = (S / GS) * NO, ks0 = (S % GS) * KS;
         pre(st);
         if constexpr (S % GS == 0) ly.init(ot, acc);
-        if constexpr (ot > 0 && S % GS < UNITS) {
-          constexpr int u = S % GS;
-          ly.epi(ot - NO + u / (NC * EP_SPLIT), (u / EP_SPLIT) % NC, u % EP_SPLIT,
-                 ly.pend[u / (NC * EP_SPLIT)]);
-        }
+        auto deferred = [&]() {
+          if constexpr (ot > 0 && S % GS < UNITS) {
+            constexpr int u = S % GS;
+            ly.epi(ot - NO + u / (NC * EPS), (u / EPS) % NC, u % EPS,
+                   ly.pend[u / (NC * EPS)]);
+          }
+        };
+        if constexpr (!PNTF_EPI_LATE) deferred();
 #pragma unroll
         for (int k = 0; k < KS; ++k)
 #pragma unroll
@@ -339,6 +385,7 @@ __device__ __forceinline__ void layer(Ring& ring, Rsrc W, int wbase, const f32x4
 #pragma unroll
               for (int c = 0; c < NC; ++c)
                 acc[o][c] = mfma(a[o * KS + k][s], in[c * KT + ks0 + k][s], acc[o][c]);
+        if constexpr (PNTF_EPI_LATE) deferred();
         if constexpr (S % GS == GS - 1) {
 #pragma unroll
           for (int o = 0; o < NO; ++o)
@@ -356,24 +403,25 @@ struct Tail {
   template <class ST>
   __device__ __forceinline__ void operator()(ST) const {
     constexpr int j = ST::value;
-    if constexpr (j < L::NO * L::NC * EP_SPLIT)
-      ly.epi(L::OT - L::NO + j / (L::NC * EP_SPLIT), (j / EP_SPLIT) % L::NC, j % EP_SPLIT,
-             ly.pend[j / (L::NC * EP_SPLIT)]);
+    if constexpr (j < L::NO * L::NC * L::EPS)
+      ly.epi(L::OT - L::NO + j / (L::NC * L::EPS), (j / L::EPS) % L::NC, j % L::EPS,
+             ly.pend[j / (L::NC * L::EPS)]);
   }
 };
 // ... or run at once.
 template <class L>
 __device__ __forceinline__ void flush(L& ly) {
   Tail<L> t{ly};
-  static_for<0, L::NO * L::NC * EP_SPLIT>([&](auto j) { t(j); });
+  static_for<0, L::NO * L::NC * L::EPS>([&](auto j) { t(j); });
 }
 
 // ---------------------------------------------------------------- layer kinds
 // Forward: out[c*OT+t] = softplus(A·in + bias (+ out[c*OT+t] if RES)); σ10(pre) saved to
 // scratch tile sc0 + c*OT + t when SAVE, and kept in keep[t] when KEEP (single column).
-template <int OT_, int KT_, int NC_, bool RES, bool SAVE, bool KEEP = false>
+template <int OT_, int KT_, int NC_, bool RES, bool SAVE, bool KEEP = false, int EPS_ = EP_SPLIT>
 struct FwdAct {
   static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_, OT_>();
+  static constexpr int EPS = EPS_, ROWS = 4 / EPS_;
   Rsrc W;
   int bias;
   f32x4 (&out)[16];
@@ -395,12 +443,12 @@ struct FwdAct {
   __device__ __forceinline__ void epi(int t, int c, int h, const f32x4 (&v)[NC]) {
     const f32x4 b = bb[(t / NO) & 1][t % NO];
 #pragma unroll
-    for (int r = h * EP_ROWS; r < (h + 1) * EP_ROWS; ++r) {
+    for (int r = h * ROWS; r < (h + 1) * ROWS; ++r) {
       SpSig q = sp_sig(v[c][r] + b[r]);
       out[c * OT + t][r] = q.sp;
       sgp[r] = q.sg;
     }
-    if (h == EP_SPLIT - 1) {
+    if (h == EPS - 1) {
       if (SAVE) store_tile(sc, sc0 + c * OT + t, lane, sgp);
       if (KEEP) keep[t] = sgp;
     }
@@ -408,9 +456,10 @@ struct FwdAct {
 };
 
 // out[c*OT+t] = A·in + bias, no activation (encoder[-1], :234).
-template <int OT_, int KT_, int NC_>
+template <int OT_, int KT_, int NC_, int EPS_ = EP_SPLIT>
 struct FwdLin {
   static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_, OT_>();
+  static constexpr int EPS = EPS_, ROWS = 4 / EPS_;
   Rsrc W;
   int bias;
   f32x4 (&out)[16];
@@ -429,36 +478,80 @@ struct FwdLin {
   __device__ __forceinline__ void epi(int t, int c, int h, const f32x4 (&v)[NC]) {
     const f32x4 b = bb[(t / NO) & 1][t % NO];
 #pragma unroll
-    for (int r = h * EP_ROWS; r < (h + 1) * EP_ROWS; ++r) out[c * OT + t][r] = v[c][r] + b[r];
+    for (int r = h * ROWS; r < (h + 1) * ROWS; ++r) out[c * OT + t][r] = v[c][r] + b[r];
   }
 };
 
 // Reverse: out[c*OT+t] = (A^T·in (+ out[c*OT+t] if RES)) ⊙ scratch[mul0 + c*OT + t] (if MUL)
-template <int OT_, int KT_, int NC_, bool RES, bool MUL>
+// The saved-σ tiles of group gi are loaded AH groups before its deferred epilogue runs: at
+// the start of group gi - AH + 1 (AH = 1: when the group itself starts).  With AH > 1 the
+// first AH - 1 groups are loaded by preload(), which the caller runs inside the previous
+// layer (Preload / At hooks), so even the layer's first group gets the full lead.
+template <int OT_, int KT_, int NC_, bool RES, bool MUL, int AH = 1, int EPS_ = EP_SPLIT>
 struct Bwd {
   static constexpr int OT = OT_, KT = KT_, NC = NC_, NO = out_group<NC_, OT_>();
+  static constexpr int EPS = EPS_, ROWS = 4 / EPS_;
+  static constexpr int NG = OT / NO, NB = AH + 1;
   f32x4 (&out)[16];
   Scratch sc;
   int mul0, lane;
-  f32x4 m[2][NO][NC];
+  f32x4 m[NB][NO][NC];
   f32x4 pend[NO][NC];
-  __device__ __forceinline__ void init(int ot, f32x4 (&acc)[NO][NC]) {
-    const int par = (ot / NO) & 1;
+  __device__ __forceinline__ void load_group(int gi) {
 #pragma unroll
     for (int o = 0; o < NO; ++o)
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        if (MUL) m[par][o][c] = load_tile(sc, mul0 + c * OT + ot + o, lane);
-        acc[o][c] = RES ? out[c * OT + ot + o] : zero4();
-      }
+      for (int c = 0; c < NC; ++c)
+        m[gi % NB][o][c] = load_tile(sc, mul0 + c * OT + gi * NO + o, lane);
+  }
+  __device__ __forceinline__ void preload() {
+    if (MUL)
+#pragma unroll
+      for (int gi = 0; gi < AH - 1; ++gi) load_group(gi);
+  }
+  __device__ __forceinline__ void init(int ot, f32x4 (&acc)[NO][NC]) {
+    const int gi = ot / NO;
+    if (MUL && gi + AH - 1 < NG) load_group(gi + AH - 1);
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[o][c] = RES ? out[c * OT + ot + o] : zero4();
   }
   __device__ __forceinline__ void epi(int t, int c, int h, const f32x4 (&v)[NC]) {
-    const f32x4 mm = m[(t / NO) & 1][t % NO][c];
+    const f32x4 mm = m[(t / NO) % NB][t % NO][c];
 #pragma unroll
-    for (int r = h * EP_ROWS; r < (h + 1) * EP_ROWS; ++r)
+    for (int r = h * ROWS; r < (h + 1) * ROWS; ++r)
       out[c * OT + t][r] = MUL ? v[c][r] * mm[r] : v[c][r];
   }
 };
+
+// Pre hooks: run f() at step N of the layer; run two hooks.
+template <int N, class F>
+struct At {
+  F f;
+  template <class ST>
+  __device__ __forceinline__ void operator()(ST) const {
+    if constexpr (ST::value == N) f();
+  }
+};
+template <int N, class F>
+__device__ __forceinline__ At<N, F> at(F f) {
+  return At<N, F>{f};
+}
+template <class A, class B>
+struct Both {
+  A a;
+  B b;
+  template <class ST>
+  __device__ __forceinline__ void operator()(ST st) const {
+    a(st);
+    b(st);
+  }
+};
+template <class A, class B>
+__device__ __forceinline__ Both<A, B> both(A a, B b) {
+  return Both<A, B>{a, b};
+}
 
 // ---------------------------------------------------------------- one pair tile
 struct PairIO {
@@ -551,10 +644,10 @@ __device__ __forceinline__ float forward_pass(Ring& ring, const float* __restric
     f32x4 bw[2][DIM];   // B rows of the lane's features, one Fourier tile ahead
 #pragma unroll
     for (int d = 0; d < DIM; ++d) bw[0][d] = ld4(io.Bw + d * H + 4 * g);
-    run_steps<64, 2, 2, SITE_FWD_E0>(
+    run_steps<64, 2, EKS, SITE_FWD_E0>(
         ring, W, lane * 16,
         [&](int st, int l) { return frag<16>(F + OFF_E0 * 4, st % 8, st / 8 + 8 * l); },
-        Head<8, 2>{F + OFF_EBLK * 4},
+        Head<8, EKS>{F + OFF_EBLK * 4},
         [&](auto st, const f32x4 (&a)[2]) {
           constexpr int S = decltype(st)::value;
           constexpr int kt = S / 8, ot = S % 8;
@@ -580,7 +673,7 @@ __device__ __forceinline__ float forward_pass(Ring& ring, const float* __restric
                 cs[c][s] = x1;
               }
           }
-          if constexpr (kt == 7 && ot > 0) e0epi(ot - 1);
+          if constexpr (kt == 7 && ot > 0 && !PNTF_EPI_LATE) e0epi(ot - 1);
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
 #pragma unroll
@@ -588,6 +681,7 @@ __device__ __forceinline__ float forward_pass(Ring& ring, const float* __restric
 #pragma unroll
             for (int c = 0; c < 2; ++c) X[c * 8 + ot] = mfma(a[1][s], cs[c][s], X[c * 8 + ot]);
           }
+          if constexpr (kt == 7 && ot > 0 && PNTF_EPI_LATE) e0epi(ot - 1);
         });
   }
   PNTF_STAMP(1);
@@ -595,30 +689,30 @@ __device__ __forceinline__ float forward_pass(Ring& ring, const float* __restric
   // ---- encoder residual blocks (:228-232), unrolled; X = h (2 cols x 8 tiles)
   const int BE = BB + B_EBLK * 4;
   const int WE = F + OFF_EBLK * 4;
-  FwdAct<8, 8, 2, false, GRAD> a0{W, BE, Y, sc, T_EBLK, lane, cy.sg3};
-  layer<8, 8, 2, 2, SITE_FWD_ENC, 2>(
+  FwdAct<8, 8, 2, false, GRAD, false, EEPS> a0{W, BE, Y, sc, T_EBLK, lane, cy.sg3};
+  layer<8, 8, 2, EKS, SITE_FWD_ENC, EKS>(
       ring, W, WE, X, lane, a0,
       [&](auto st) {
         if constexpr (decltype(st)::value == 0) e0epi(7);
       },
-      Head<8, 2>{WE + SZ_E * 4});
+      Head<8, EKS>{WE + SZ_E * 4});
   PNTF_STAMP(2);
-  FwdAct<8, 8, 2, true, GRAD> b0{W, BE + 128 * 4, X, sc, T_EBLK + 16, lane, cy.sg3};
-  layer<8, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + SZ_E * 4, Y, lane, b0, Tail<decltype(a0)>{a0},
-                                  Head<8, 2>{WE + 2 * SZ_E * 4});
+  FwdAct<8, 8, 2, true, GRAD, false, EEPS> b0{W, BE + 128 * 4, X, sc, T_EBLK + 16, lane, cy.sg3};
+  layer<8, 8, 2, EKS, SITE_FWD_ENC, EKS>(ring, W, WE + SZ_E * 4, Y, lane, b0,
+                                      Tail<decltype(a0)>{a0}, Head<8, EKS>{WE + 2 * SZ_E * 4});
   PNTF_STAMP(3);
-  FwdAct<8, 8, 2, false, GRAD> a1{W, BE + 256 * 4, Y, sc, T_EBLK + 32, lane, cy.sg3};
-  layer<8, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
-                                  Tail<decltype(b0)>{b0}, Head<8, 2>{WE + 3 * SZ_E * 4});
+  FwdAct<8, 8, 2, false, GRAD, false, EEPS> a1{W, BE + 256 * 4, Y, sc, T_EBLK + 32, lane, cy.sg3};
+  layer<8, 8, 2, EKS, SITE_FWD_ENC, EKS>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
+                                      Tail<decltype(b0)>{b0}, Head<8, EKS>{WE + 3 * SZ_E * 4});
   PNTF_STAMP(4);
-  FwdAct<8, 8, 2, true, GRAD> b1{W, BE + 384 * 4, X, sc, T_EBLK + 48, lane, cy.sg3};
-  layer<8, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
-                                  Tail<decltype(a1)>{a1}, Head<8, 2>{F + OFF_E3 * 4});
+  FwdAct<8, 8, 2, true, GRAD, false, EEPS> b1{W, BE + 384 * 4, X, sc, T_EBLK + 48, lane, cy.sg3};
+  layer<8, 8, 2, EKS, SITE_FWD_ENC, EKS>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
+                                      Tail<decltype(a1)>{a1}, Head<8, EKS>{F + OFF_E3 * 4});
   PNTF_STAMP(5);
   // ---- encoder[-1] (:234) -> Y (zs = Y[0..7], zg = Y[8..15])
-  FwdLin<8, 8, 2> e3{W, BB + B_E3 * 4, Y, lane};
-  layer<8, 8, 2, 2, SITE_FWD_ENC, 4>(ring, W, F + OFF_E3 * 4, X, lane, e3, Tail<decltype(b1)>{b1},
-                                  Head<16>{F + OFF_GBLK * 4});
+  FwdLin<8, 8, 2, EEPS> e3{W, BB + B_E3 * 4, Y, lane};
+  layer<8, 8, 2, EKS, SITE_FWD_ENC, 4>(ring, W, F + OFF_E3 * 4, X, lane, e3,
+                                    Tail<decltype(b1)>{b1}, Head<16>{F + OFF_GBLK * 4});
   flush(e3);
   PNTF_STAMP(6);
 
@@ -713,6 +807,17 @@ __device__ __forceinline__ void backward_pass(Ring& ring, const float* __restric
   for (int t = 0; t < 8; ++t) s0t[t] = load_tile(sc, T_S0 + t, lane);
 #endif
 
+  // encoder reverse layers (constructed here: each one's first σ groups are preloaded inside
+  // the layer before it, PNTF_ENC_AH groups ahead of their use)
+  const int WE = Bk + OFF_EBLK * 4;
+  constexpr int EAH = PNTF_ENC_AH;
+  Bwd<8, 8, 2, false, true, EAH, EEPS> e3{Y, sc, T_EBLK + 32 * 1 + 16, lane};
+  Bwd<8, 8, 2, false, true, EAH, EEPS> b1{X, sc, T_EBLK + 32, lane};
+  Bwd<8, 8, 2, true, true, EAH, EEPS> a1{Y, sc, T_EBLK + 16, lane};
+  Bwd<8, 8, 2, false, true, EAH, EEPS> b0{X, sc, T_EBLK, lane};
+  Bwd<8, 8, 2, true, true, EAH, EEPS> a0{Y, sc, T_E0, lane};
+  constexpr int ELAST = 7 * EGS;   // first step of an encoder layer's last group (of 8)
+
   // ---- generator blocks, reverse (:615-618)
 #pragma unroll 1
   for (int i = 2; i >= 0; --i) {
@@ -730,8 +835,11 @@ __device__ __forceinline__ void backward_pass(Ring& ring, const float* __restric
       flush(la);
     } else {
       Bwd<16, 16, 1, true, false> la{X, sc, 0, lane};
-      layer<16, 16, 1, 1, SITE_BWD_GEN, 2>(ring, W, wa, Y, lane, la, Tail<decltype(lb)>{lb},
-                                        Head<8, 2>{Bk + OFF_E3 * 4});
+      // its last group (4 out tiles x 16 steps) starts at step 48: preload e3's first σ there
+      layer<16, 16, 1, 1, SITE_BWD_GEN, EKS>(ring, W, wa, Y, lane, la,
+                                          both(Tail<decltype(lb)>{lb},
+                                               at<48>([&] { e3.preload(); })),
+                                          Head<8, EKS>{Bk + OFF_E3 * 4});
       flush(la);
     }
   }
@@ -752,28 +860,29 @@ __device__ __forceinline__ void backward_pass(Ring& ring, const float* __restric
   }
   PNTF_STAMP(25);
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1) -> Y
-  const int WE = Bk + OFF_EBLK * 4;
-  Bwd<8, 8, 2, false, true> e3{Y, sc, T_EBLK + 32 * 1 + 16, lane};
-  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, Bk + OFF_E3 * 4, X, lane, e3, NoPre{},
-                                  Head<8, 2>{WE + 3 * SZ_E * 4});
+  layer<8, 8, 2, EKS, SITE_BWD_ENC, EKS>(ring, W, Bk + OFF_E3 * 4, X, lane, e3,
+                                      at<ELAST>([&] { b1.preload(); }),
+                                      Head<8, EKS>{WE + 3 * SZ_E * 4});
   PNTF_STAMP(26);
   // ---- encoder blocks, reverse (:633-636), unrolled
   // da = (E1_b^T dr) ⊙ σ10(y1_b)
-  Bwd<8, 8, 2, false, true> b1{X, sc, T_EBLK + 32, lane};
-  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
-                                  Tail<decltype(e3)>{e3}, Head<8, 2>{WE + 2 * SZ_E * 4});
+  layer<8, 8, 2, EKS, SITE_BWD_ENC, EKS>(
+      ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
+      both(Tail<decltype(e3)>{e3}, at<ELAST>([&] { a1.preload(); })),
+      Head<8, EKS>{WE + 2 * SZ_E * 4});
   PNTF_STAMP(27);
   // dh = E_b^T da + dr, then ⊙ σ10 of the layer below (block 0's y2, or encoder[0])
-  Bwd<8, 8, 2, true, true> a1{Y, sc, T_EBLK + 16, lane};
-  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
-                                  Tail<decltype(b1)>{b1}, Head<8, 2>{WE + 1 * SZ_E * 4});
+  layer<8, 8, 2, EKS, SITE_BWD_ENC, EKS>(
+      ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
+      both(Tail<decltype(b1)>{b1}, at<ELAST>([&] { b0.preload(); })),
+      Head<8, EKS>{WE + 1 * SZ_E * 4});
   PNTF_STAMP(28);
-  Bwd<8, 8, 2, false, true> b0{X, sc, T_EBLK, lane};
-  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0,
-                                  Tail<decltype(a1)>{a1}, Head<8, 2>{WE});
+  layer<8, 8, 2, EKS, SITE_BWD_ENC, EKS>(
+      ring, W, WE + 1 * SZ_E * 4, Y, lane, b0,
+      both(Tail<decltype(a1)>{a1}, at<ELAST>([&] { a0.preload(); })), Head<8, EKS>{WE});
   PNTF_STAMP(29);
-  Bwd<8, 8, 2, true, true> a0{Y, sc, T_E0, lane};
-  layer<8, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE, X, lane, a0, Tail<decltype(b0)>{b0}, FoldHead{});
+  layer<8, 8, 2, EKS, SITE_BWD_ENC, 2>(ring, W, WE, X, lane, a0, Tail<decltype(b0)>{b0},
+                                    FoldHead{});
   PNTF_STAMP(30);
 
   // ---- encoder[0]^T (256 x 128: OT 16, KT 8) fused with the Fourier Jacobian (:639-645)
@@ -816,7 +925,7 @@ __device__ __forceinline__ void backward_pass(Ring& ring, const float* __restric
 #pragma unroll
           for (int d = 0; d < DIM; ++d) bw[p][d] = ld4(io.Bw + d * H + 16 * kf + 4 * g);
         }
-        if constexpr (kf > 0 && kt < 2) fold(kf - 1, kt);
+        if constexpr (kf > 0 && kt < 2 && !PNTF_EPI_LATE) fold(kf - 1, kt);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -824,6 +933,7 @@ __device__ __forceinline__ void backward_pass(Ring& ring, const float* __restric
             ph[p][0][c] = mfma(a[0][s], Y[c * 8 + kt][s], ph[p][0][c]);
             ph[p][1][c] = mfma(a[1][s], Y[c * 8 + kt][s], ph[p][1][c]);
           }
+        if constexpr (kf > 0 && kt < 2 && PNTF_EPI_LATE) fold(kf - 1, kt);
       });
   fold(7, 0);
   fold(7, 1);

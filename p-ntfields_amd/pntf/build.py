@@ -40,6 +40,27 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + INCLU
             "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
             "-save-temps=obj", "-Rpass-analysis=kernel-resource-usage"]
 PACKED_FP32 = re.compile(r"\bv_pk_(mul|add|fma)_f32\b")
+# saved-σ scratch: the stores and loads of a wave's slot go through one buffer descriptor
+SCRATCH_STORE = re.compile(r"buffer_store_dwordx4 v\[\d+:\d+\], v\d+, (s\[\d+:\d+\])[^\n]*\bnt\b")
+BUFFER_LOAD = re.compile(r"buffer_load_dwordx4 v\[\d+:\d+\], v\d+, (s\[\d+:\d+\])([^\n]*)")
+# units whose kernels keep a saved-σ scratch slot (τ-only / travel-time kernels have none)
+SCRATCH_UNITS = re.compile(r"^(field_d\d_k[123]|fsplit_d\d_k[123]|plan_.*|residual_d\d)$")
+
+
+def scratch_policy_violations(asm):
+    """Stale-L1 guard.  A persistent wave rewrites its scratch slot for every
+    tile and its stores do not refresh the CU's vector L1, so every load through the scratch
+    descriptor (the one the nt stores use) must carry the nt policy (bypass L1).  Returns
+    (scratch descriptors, nt loads through them, loads through them without nt)."""
+    descs = set(SCRATCH_STORE.findall(asm))
+    good = bad = 0
+    for m in BUFFER_LOAD.finditer(asm):
+        if m.group(1) in descs:
+            if re.search(r"\bnt\b", m.group(2)):
+                good += 1
+            else:
+                bad += 1
+    return descs, good, bad
 
 UNITS = (
     [("field_d%d_k%d" % (d, k), "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k])
@@ -134,6 +155,12 @@ def _compile(unit):
             m = PACKED_FP32.search(fh.read())
         if m:
             raise RuntimeError("packed-fp32 op %s in %s (hazard guard)" % (m.group(0), asm))
+        if SCRATCH_UNITS.match(name):
+            with open(asm) as fh:
+                descs, good, bad = scratch_policy_violations(fh.read())
+            if not descs or not good or bad:
+                raise RuntimeError("scratch-slot policy guard in %s: descriptors %s, %d nt "
+                                   "loads, %d loads without nt" % (asm, descs, good, bad))
     for f in glob.glob(os.path.join(d, "*")):
         if not f.endswith((".o", ".s")):
             os.remove(f)

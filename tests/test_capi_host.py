@@ -180,18 +180,33 @@ def _asm(unit):
     return open(files[0]).read()
 
 
-@pytest.mark.parametrize("unit", ["field_d3_k1", "field_d6_k1", "plan_d6", "fsplit_d3_k1"])
+@pytest.mark.parametrize("unit", ["field_d3_k1", "field_d6_k1", "plan_d6", "fsplit_d3_k1",
+                                  "residual_d3"])
 def test_scratch_reloads_bypass_l1(unit):
     """Regression guard for DESIGN §7.3: a persistent wave rewrites its saved-σ slot for every
     tile and its stores do not refresh the CU's L1, so every load through the scratch buffer
-    resource must carry the `nt` policy (a build without it returned stale σ tiles)."""
-    asm = _asm(unit)
-    op = r"\s+v\[?[\d:]+\]?,\s+v\d+,\s+(s\[\d+:\d+\]),"     # data, voffset, resource
-    stores = re.findall(r"buffer_store_dwordx4" + op, asm)
-    assert stores, "no scratch stores found"
-    assert all(" nt" in l for l in re.findall(r"buffer_store_dwordx4.*", asm))
-    res = set(stores)
-    loads = [l for l in re.findall(r"buffer_load_dwordx4" + op + "(.*)", asm) if l[0] in res]
-    assert len(loads) >= len(re.findall(r"buffer_store_dwordx4", asm))
-    bad = [l for l in loads if not l[1].rstrip().endswith(" nt")]
-    assert not bad, bad[:3]
+    resource must carry the `nt` policy (a build without it returned stale σ tiles).  The same
+    check runs inside pntf.build for every scratch-holding unit and fails the build."""
+    from pntf import build
+    descs, good, bad = build.scratch_policy_violations(_asm(unit))
+    assert descs and good > 0 and bad == 0, (descs, good, bad)
+
+
+def test_scratch_guard_catches_a_build_without_nt_loads(tmp_path):
+    """A build variant whose scratch loads drop the nt bit (-DPNTF_SCRATCH_LOAD_AUX=0) must be
+    rejected by the build guard: compile the split τ+∇τ kernel that way (device code only) and
+    check that the guard counts its scratch loads as violations."""
+    import subprocess
+    from pntf import build
+    out = str(tmp_path / "variant.s")
+    cmd = ([build.hipcc()] + [f for f in build.CXXFLAGS if not f.startswith(("-save-temps",
+                                                                            "-Rpass"))]
+           + ["-DPNTF_DIM=3", "-DPNTF_KIND=1", "-DPNTF_SPLIT_FIELD",
+              "-DPNTF_SCRATCH_LOAD_AUX=0", "--cuda-device-only", "-S",
+              os.path.join(build.CSRC, "pntf_kernels.hip"), "-o", out])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0 and "not found" in r.stderr:
+        pytest.skip("hipcc unavailable")
+    assert r.returncode == 0, r.stderr[-2000:]
+    descs, good, bad = build.scratch_policy_violations(open(out).read())
+    assert descs and bad > 0 and good == 0, (descs, good, bad)

@@ -294,3 +294,62 @@ def test_field_grid_vs_oracle():
     assert _rel(TT.ravel(), O.travel_time(xp, t)) < 1e-4
     assert _rel(V.ravel(), O.speed(xp, t, d)) < 1e-3
     assert md is not None
+
+
+def _write_arm_dataset(path, N=30000):
+    from models import data_mlp as dbm
+    pts = synth.make_box_pairs(N, 6, seed=90)
+    return dbm.write_dataset(path, pts, synth.make_speeds(N, seed=91)), pts
+
+
+def test_arm_database_format_roundtrip(tmp_path):
+    """models/data_mlp.py:8-43: [points | speed] fp32 rows; the packed 128^3 occupancy grid is
+    read (and unpacked) like the reference."""
+    from models import data_mlp as dbm
+    occ = np.zeros((128,) * 3, bool)
+    occ[3, 5, 7] = True
+    path, pts = str(tmp_path / "arm"), synth.make_box_pairs(100, 6, seed=92)
+    dbm.write_dataset(path, pts, synth.make_speeds(100, seed=93), occ)
+    ds = dbm.Database(path)
+    assert ds.data.shape == (100, 14) and ds.data.dtype == torch.float32 and len(ds) == 100
+    assert np.array_equal(ds.data[:, :12].numpy(), pts)
+    assert np.array_equal(ds.data[:, 12:].numpy(), synth.make_speeds(100, seed=93))
+    with np.load(str(tmp_path / "arm" / dbm.GRID_FILE)) as z:
+        assert np.unpackbits(z["compressed_occupancies"]).reshape((128,) * 3)[3, 5, 7] == 1
+
+
+def test_arm_fast_loader_batches():
+    """FastTensorDataLoader (models/model_res_sigmoid.py:30-73): ceil(N/bs) batches that
+    cover a permutation of the rows."""
+    from models import model_res_sigmoid as ma
+    t = torch.arange(25, dtype=torch.float32).unsqueeze(1)
+    dl = ma.FastTensorDataLoader(t, batch_size=10, shuffle=True)
+    assert len(dl) == 3
+    rows = torch.cat([b[0] for b in dl]).squeeze(1)
+    assert sorted(rows.tolist()) == list(range(25))
+
+
+@pytest.mark.gpu
+def test_arm_model_train_two_epochs(tmp_path):
+    """Arm Model.train (models/model_res_sigmoid.py:938-1137) end to end over a data_mlp
+    dataset: finite losses, the 6-batch epoch cap, checkpoints that restore B, plots."""
+    from models import model_res_sigmoid as ma
+    path, _ = _write_arm_dataset(str(tmp_path / "arm"))
+    mp = tmp_path / "ckpt"
+    mp.mkdir()
+    torch.manual_seed(0)
+    model = ma.Model(str(mp), path, 6, device="cuda:0")
+    model.Params["Training"]["Number of Epochs"] = 2
+    model.train()
+    assert len(model.total_train_loss) == 2
+    assert all(np.isfinite(float(v)) for v in model.total_train_loss)
+    files = sorted(p.name for p in mp.iterdir() if p.suffix == ".pt")
+    assert len(files) == 2 and files[0].startswith("Model_Epoch_00001_")
+    assert len([p for p in mp.iterdir() if p.suffix == ".jpg"]) == 4
+    m2 = ma.Model(str(mp), path, 6, device="cuda:0")
+    m2.load(str(mp / files[-1]))
+    assert torch.equal(m2.B.cpu(), model.B.cpu())
+    for (k, a), b in zip(model.network.state_dict().items(), m2.network.state_dict().values()):
+        assert torch.equal(a.cpu(), b.cpu()), k
+    xp = torch.from_numpy(synth.make_box_pairs(64, 6, seed=94)).cuda()
+    assert torch.equal(model.Gradient(xp), m2.Gradient(xp))

@@ -9,8 +9,9 @@ GPU (BASELINE.json metric).
 (pntf/launch.py: one fresh interpreter per GPU, before anything touches the GPU); under
 torchrun the ranks come from the environment and WORLD_SIZE must equal N.
 
-One step = the fused HIP τ+∇τ kernel (exact reverse mode, = Model.gradient(NN.out)) over the
-rank's resident batch of synthetic Gibson-shaped pairs (10 environments, per-pair env id),
+One step = the fused HIP τ+∇τ kernel (exact reverse mode, = Model.gradient(NN.out); at this
+size AUTO picks the 32-pair wide kernel, pntf_wide.h) over the rank's resident batch of
+synthetic Gibson-shaped pairs (10 environments, per-pair env id),
 followed for N > 1 by the RCCL all-gather of every rank's τ+∇τ rows (the multi-GPU exchange
 the north star names).  Weak scaling by default (--pairs per rank); --total-pairs T splits a
 fixed total over the ranks instead (strong scaling).  Rank 0 prints one JSON line; `value` =
@@ -44,7 +45,7 @@ BYTES_PER_PAIR = 52                # 24 B in + 4 B tau + 24 B dtau (algorithmic 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: Peak FP32 (matrix)
 METRIC = "(start,goal) tau+grad-tau evals/sec at batch=1M, Gibson 3D"
 UNIT = "pairs/s"
-HEADLINE_UNIT = "field_d3_k1"      # build unit of field_kernel<3, K_TAU_GRAD> (pntf/build.py)
+HEADLINE_UNIT = "wide_d3_k1"       # build unit of wide_field_kernel<3, K_TAU_GRAD> (pntf/build.py)
 
 
 def parse(argv=None):
@@ -266,7 +267,7 @@ def run(args):
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "field_kernel<3,K_TAU_GRAD>", "unit_hash": unit_hash,
+                         "kernel": "wide_field_kernel<3,K_TAU_GRAD>", "unit_hash": unit_hash,
                          "kernel_ms": kern_ms, "kernel_ms_min": float(kms.min()),
                          "kernel_ms_max": float(kms.max()), "launches_timed": R,
                          "flop_per_pair": FLOP_PER_PAIR,
@@ -331,6 +332,14 @@ def extras(packed, dev):
     out["c2_tau_only_262144_pairs_per_s"] = n2 / (ms * 1e-3)
     ms = timeit(lambda: ops.path_velocity(packed, xp, B, dim=3))
     out["c2_path_velocity_262144_pairs_per_s"] = n2 / (ms * 1e-3)
+    # the headline batch on the 16-pair kernel (pntf_field.h), for comparison with the wide one
+    n1 = 1 << 20
+    xh = torch.from_numpy(synth.make_pairs(n1, 3, seed=1000)).to(dev)
+    Bh = torch.from_numpy(synth.make_B_table(10, 3)).to(dev)
+    eh = torch.from_numpy(synth.make_env_ids(n1, 10)).to(dev)
+    out["headline_1M_wave_tile_kernel_ms"] = timeit(
+        lambda: ops.tau_grad(packed, xh, Bh, eh, dim=3, schedule="wave_tile"), reps=3)
+    del xh, eh
     # C1 shape on the GPU (4096 pairs, latency-bound): split tiles vs one wave per tile
     x1 = torch.from_numpy(synth.make_pairs(4096, 3, seed=2)).to(dev)
     for sched in ("auto", "wave_tile"):

@@ -42,12 +42,18 @@ typedef enum {
 /* Gradient flavours for the reverse sweep. */
 #define PNTF_GRAD_EXACT 0            /* == Model.gradient(NN.out) autograd (:890-896)     */
 #define PNTF_GRAD_BACKGRAD_COMPAT 1  /* == NN.out_backgrad incl. its encoder[0] quirk     */
+                                     /*    (model_res_sigmoid_multi.py:402-647, :435-438) */
 
-/* Planner schedules (pntf_plan_ex). */
+/* Kernel schedules (pntf_field_ex, pntf_plan_ex, pntf_set_field_schedule):
+ *   WAVE_TILE   one wave per 16-pair tile, v_mfma_f32_16x16x4_f32 (pntf_field.h);
+ *   SPLIT_TILE  the 4 waves of a workgroup share a 16-pair tile (pntf_split.h; latency);
+ *   WIDE_TILE   one wave per 32-pair tile, v_mfma_f32_32x32x2_f32 (pntf_wide.h; throughput,
+ *               field entry points only — the planner treats it as WAVE_TILE);
+ *   AUTO        split while ceil(n/16) <= 2 x the CU count, wide above. */
 #define PNTF_SCHED_AUTO 0
 #define PNTF_SCHED_WAVE_TILE 1
 #define PNTF_SCHED_SPLIT_TILE 2
-                                     /*    (model_res_sigmoid_multi.py:402-647, :435-438) */
+#define PNTF_SCHED_WIDE_TILE 3
 
 int pntf_abi_version(void);
 const char* pntf_status_string(int status);

@@ -14,6 +14,8 @@ template <int DIM, int KIND>
 __global__ void field_kernel(FieldArgs a);
 template <int DIM, int KIND>
 __global__ void field_split_kernel(FieldArgs a);
+template <int DIM, int KIND>
+__global__ void wide_field_kernel(FieldArgs a);
 template <int DIM>
 __global__ void plan_kernel(PlanArgs a);
 template <int DIM>
@@ -24,6 +26,9 @@ __global__ void sum_kernel(const float* __restrict__ x, int64_t n, double* __res
 __global__ void pack_kernel(const float* __restrict__ src, int rows, int cols, int ld,
                             int trans, float* __restrict__ dst);
 __global__ void copy_kernel(const float* __restrict__ src, int n, float* __restrict__ dst);
+__global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int cols, int ld,
+                                 int trans, float* __restrict__ dst);
+__global__ void pack_wide_aux_kernel(const float* __restrict__ plain, float* __restrict__ wide);
 }  // namespace pntf
 
 using namespace pntf;
@@ -54,6 +59,7 @@ static int num_cus() {
 }
 
 static constexpr size_t SLOT_BYTES = (size_t)SCRATCH_FLOATS_PER_WAVE * sizeof(float);
+static constexpr size_t WSLOT_BYTES = (size_t)WSCRATCH_FLOATS_PER_WAVE * sizeof(float);
 
 // persistent grid: one 4-wave workgroup per CU at most, never more than the tiles need
 static int64_t grid_for(int64_t n) {
@@ -70,9 +76,18 @@ static int64_t split_grid_for(int64_t n) {
   return ntiles < cap ? (ntiles < 1 ? 1 : ntiles) : cap;
 }
 
-static int grid_with_ws(int64_t n, size_t ws_bytes, int64_t* grid, bool split = false) {
-  int64_t g = split ? split_grid_for(n) : grid_for(n);
-  int64_t fit = (int64_t)(ws_bytes / (SLOT_BYTES * WAVES));
+// wide grid (pntf_wide.h): 32-pair tiles, one 4-wave workgroup per CU at most
+static int64_t wide_grid_for(int64_t n) {
+  int64_t ntiles = (n + WTILE - 1) / WTILE;
+  int64_t wgs = (ntiles + WAVES - 1) / WAVES;
+  int64_t cap = (int64_t)num_cus() * WG_PER_CU;
+  return wgs < cap ? (wgs < 1 ? 1 : wgs) : cap;
+}
+
+static int grid_with_ws(int64_t n, size_t ws_bytes, int64_t* grid, bool split = false,
+                        bool wide = false) {
+  int64_t g = split ? split_grid_for(n) : wide ? wide_grid_for(n) : grid_for(n);
+  int64_t fit = (int64_t)(ws_bytes / ((wide ? WSLOT_BYTES : SLOT_BYTES) * WAVES));
   if (fit < 1) return fail(PNTF_ERR_WORKSPACE, "workspace too small (%s)", "need >= 4 slots");
   *grid = g < fit ? g : fit;
   return PNTF_OK;
@@ -83,7 +98,7 @@ static int grid_with_ws(int64_t n, size_t ws_bytes, int64_t* grid, bool split = 
 // win once the tiles fill every SIMD.
 static bool use_split(int64_t n, int schedule) {
   if (schedule == PNTF_SCHED_SPLIT_TILE) return true;
-  if (schedule == PNTF_SCHED_WAVE_TILE) return false;
+  if (schedule == PNTF_SCHED_WAVE_TILE || schedule == PNTF_SCHED_WIDE_TILE) return false;
   return (n + TILE - 1) / TILE <= 2 * (int64_t)num_cus();
 }
 
@@ -92,7 +107,8 @@ static bool use_split(int64_t n, int schedule) {
 static int g_field_schedule = PNTF_SCHED_AUTO;
 
 static bool valid_schedule(int s) {
-  return s == PNTF_SCHED_AUTO || s == PNTF_SCHED_WAVE_TILE || s == PNTF_SCHED_SPLIT_TILE;
+  return s == PNTF_SCHED_AUTO || s == PNTF_SCHED_WAVE_TILE || s == PNTF_SCHED_SPLIT_TILE ||
+         s == PNTF_SCHED_WIDE_TILE;
 }
 
 #ifndef PNTF_BUILD_INFO
@@ -113,8 +129,22 @@ static int check_common(const float* packed, int dim, const float* xp, int64_t n
 
 template <int DIM>
 static void launch_field(int kind, int64_t grid, const FieldArgs& a, hipStream_t s,
-                         bool split) {
+                         bool split, bool wide) {
   dim3 g((unsigned)grid), b(256);
+  if (wide) {
+    switch (kind) {
+      case K_TAU: hipLaunchKernelGGL((wide_field_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
+      case K_TAU_GRAD:
+        hipLaunchKernelGGL((wide_field_kernel<DIM, K_TAU_GRAD>), g, b, 0, s, a);
+        break;
+      case K_VELOCITY:
+        hipLaunchKernelGGL((wide_field_kernel<DIM, K_VELOCITY>), g, b, 0, s, a);
+        break;
+      case K_SPEED: hipLaunchKernelGGL((wide_field_kernel<DIM, K_SPEED>), g, b, 0, s, a); break;
+      default: hipLaunchKernelGGL((wide_field_kernel<DIM, K_TRAVEL>), g, b, 0, s, a); break;
+    }
+    return;
+  }
   if (split) {
     switch (kind) {
       case K_TAU: hipLaunchKernelGGL((field_split_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
@@ -152,16 +182,17 @@ static int run_field(int kind, const float* packed, int dim, const float* xp, in
   if (!out0 || (kind == K_TAU_GRAD && !out1)) return fail(PNTF_ERR_ARG, "null output%s");
   const bool grad = kind != K_TAU && kind != K_TRAVEL;
   const bool split = use_split(n, schedule);
-  int64_t grid = split ? split_grid_for(n) : grid_for(n);
+  const bool wide = !split && schedule != PNTF_SCHED_WAVE_TILE;
+  int64_t grid = split ? split_grid_for(n) : wide ? wide_grid_for(n) : grid_for(n);
   if (grad) {
     if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
-    st = grid_with_ws(n, ws_bytes, &grid, split);
+    st = grid_with_ws(n, ws_bytes, &grid, split, wide);
     if (st) return st;
   }
   FieldArgs a{packed, xp, Btab, env, n, n_env, mode, out0, out1, (float*)ws};
-  if (dim == 3) launch_field<3>(kind, grid, a, s, split);
-  else launch_field<6>(kind, grid, a, s, split);
-  return check_launch(split ? "field_split_kernel" : "field_kernel");
+  if (dim == 3) launch_field<3>(kind, grid, a, s, split, wide);
+  else launch_field<6>(kind, grid, a, s, split, wide);
+  return check_launch(split ? "field_split_kernel" : wide ? "wide_field_kernel" : "field_kernel");
 }
 
 extern "C" {
@@ -180,7 +211,7 @@ const char* pntf_status_string(int status) {
 
 const char* pntf_last_error(void) { return g_err; }
 
-size_t pntf_packed_floats(void) { return (size_t)PACKED_FLOATS; }
+size_t pntf_packed_floats(void) { return (size_t)PACKED_TOTAL; }
 
 const char* pntf_build_info(void) { return PNTF_BUILD_INFO; }
 
@@ -193,7 +224,9 @@ int pntf_set_field_schedule(int schedule) {
 size_t pntf_workspace_bytes(int64_t n) {
   if (n <= 0) n = 1;
   int64_t g = grid_for(n), gs = split_grid_for(n);
-  return (size_t)(g > gs ? g : gs) * WAVES * SLOT_BYTES;
+  size_t narrow = (size_t)(g > gs ? g : gs) * WAVES * SLOT_BYTES;
+  size_t wide = (size_t)wide_grid_for(n) * WAVES * WSLOT_BYTES;
+  return narrow > wide ? narrow : wide;
 }
 
 int pntf_pack_weights(const float* const* params, int n_params, float* packed,
@@ -219,7 +252,7 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
       {28, 256, 256, OFF_GBLK + 5 * SZ_G},                    // generator1.2
       {20, 128, 256, OFF_G3},                                 // generator.3
   };
-  hipMemsetAsync(packed, 0, sizeof(float) * PACKED_FLOATS, stream);
+  hipMemsetAsync(packed, 0, sizeof(float) * PACKED_TOTAL, stream);
   for (int m = 0; m < (int)(sizeof(mats) / sizeof(mats[0])); ++m) {
     const M& d = mats[m];
     int64_t cnt = (int64_t)d.rows * d.cols;
@@ -229,6 +262,11 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
                        d.cols, d.cols, 0, packed + OFF_FWD + d.off);
     hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx], d.cols,
                        d.rows, d.cols, 1, packed + OFF_BWD + d.off);
+    // the wide (32x32x2) fragment order of the same two matrices
+    hipLaunchKernelGGL(pack_wide_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx],
+                       d.rows, d.cols, d.cols, 0, packed + OFF_WIDE + OFF_FWD + d.off);
+    hipLaunchKernelGGL(pack_wide_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx],
+                       d.cols, d.rows, d.cols, 1, packed + OFF_WIDE + OFF_BWD + d.off);
   }
   struct Bc { int idx, n, off; };
   const Bc bs[] = {
@@ -240,6 +278,9 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
   for (int i = 0; i < (int)(sizeof(bs) / sizeof(bs[0])); ++i)
     hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(256), 0, stream, params[bs[i].idx], bs[i].n,
                        packed + OFF_BIAS + bs[i].off);
+  const int aux = W_SZ_BCOL + W_SZ_G4W + 4;
+  hipLaunchKernelGGL(pack_wide_aux_kernel, dim3((aux + 255) / 256), dim3(256), 0, stream,
+                     packed + OFF_BIAS, packed + OFF_WIDE);
   return check_launch("pack_weights");
 }
 

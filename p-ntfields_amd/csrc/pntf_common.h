@@ -55,7 +55,19 @@ constexpr int B_G3 = B_GBLK + 6 * 256;
 constexpr int B_G4W = B_G3 + 128;             // generator.4.weight (1 x 128)
 constexpr int B_G4B = B_G4W + 128;            // generator.4.bias (padded to 4)
 constexpr int SZ_BIAS = B_G4B + 4;
-constexpr int PACKED_FLOATS = OFF_BIAS + SZ_BIAS;
+constexpr int PACKED_FLOATS = OFF_BIAS + SZ_BIAS;   // the 16x16 ("narrow") blob
+// Wide blob (pntf_wide.h, v_mfma_f32_32x32x2_f32), packed right after the narrow one: the
+// same 13 matrices in both directions in wide fragment order (same OFF_* offsets), the bias
+// columns (one fragment per 4 out tiles of 32, bias in lanes 0-31), the head vector in the
+// 32-row register order, and the head bias.
+constexpr int OFF_WIDE = PACKED_FLOATS;
+constexpr int W_OFF_BCOL = 2 * SZ_DIR;
+constexpr int W_SZ_BCOL = (B_G4W / 128) * 256;
+constexpr int W_OFF_G4W = W_OFF_BCOL + W_SZ_BCOL;
+constexpr int W_SZ_G4W = 16 * 256;
+constexpr int W_OFF_G4B = W_OFF_G4W + W_SZ_G4W;
+constexpr int W_SZ = W_OFF_G4B + 4;
+constexpr int PACKED_TOTAL = OFF_WIDE + W_SZ;
 
 // ---------------------------------------------------------------- per-wave scratch (saved σ10)
 // Each saved "tile" is 16 feature rows x 16 pairs = 256 floats, stored lane-major
@@ -67,6 +79,16 @@ constexpr int T_GBLK = 88;                    // block i (0..2): +32i: y1 (16), 
 constexpr int T_G3 = 184;                     // 8 tiles
 constexpr int SCRATCH_TILES = 192;
 constexpr int SCRATCH_FLOATS_PER_WAVE = SCRATCH_TILES * 256;
+// Wide kernels: 32 pairs per wave; a saved tile is 32 features x 32 pairs = 4 KiB, index
+// c·OT + t for 2-point layers.
+constexpr int WTILE = 32;
+constexpr int WT_E0 = 0;                      // 2 points x 4 tiles
+constexpr int WT_EBLK = 8;                    // block b: +16b: y1 (8 tiles), y2 (8 tiles)
+constexpr int WT_S0 = 40;                     // merge switch, 4 tiles
+constexpr int WT_GBLK = 44;                   // block i: +16i: y1 (8), y2 (8)
+constexpr int WT_G3 = 92;                     // 4 tiles
+constexpr int WSCRATCH_TILES = 96;
+constexpr int WSCRATCH_FLOATS_PER_WAVE = WSCRATCH_TILES * 1024;
 
 // ---------------------------------------------------------------- kernel arguments
 enum Kind { K_TAU = 0, K_TAU_GRAD = 1, K_VELOCITY = 2, K_SPEED = 3, K_TRAVEL = 4 };

@@ -25,6 +25,7 @@ namespace pntf {
 template <int OT_, int KT_, bool RES, bool ACT, int NOUT>
 struct TaylorL {
   static constexpr int OT = OT_, KT = KT_, NC = 2, NO = 1;
+  static constexpr int EPS = EP_SPLIT, ROWS = 4 / EP_SPLIT;
   f32x4 (&out)[NOUT];
   Scratch sc;
   int sig0, lane;
@@ -38,7 +39,7 @@ struct TaylorL {
   __device__ __forceinline__ void epi(int t, int c, int h, const f32x4 (&v)[2]) {
     const f32x4 gg = g[t & 1];
 #pragma unroll
-    for (int r = h * EP_ROWS; r < (h + 1) * EP_ROWS; ++r) {
+    for (int r = h * ROWS; r < (h + 1) * ROWS; ++r) {
       const float J = v[0][r], L = v[1][r];
       if (!ACT)
         out[c * OT + t][r] = v[c][r];

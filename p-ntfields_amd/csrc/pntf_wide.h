@@ -1,0 +1,627 @@
+#pragma once
+// Wide τ / ∇τ kernels: 32 (start, goal) pairs per wave on v_mfma_f32_32x32x2_f32
+// ("wide kernels").
+//
+// Why: beside fp32 MFMAs on gfx950 every vector-memory instruction steals MFMA issue cycles
+// (tests/diag/vmem_probe.hip, mfma32_probe.hip: ~5-15 cycles per buffer_load_dwordx4 beside
+// v_mfma_f32_16x16x4_f32, ~1 beside v_mfma_f32_32x32x2_f32), and the 16-pair kernel of
+// pntf_field.h loads one 1 KiB weight fragment per 4-8 of its MFMAs.  With 32 pairs as the
+// MFMA's N dimension one fragment feeds 4 (32x32x2) MFMAs of 64 cycles, so the weight stream
+// costs half the loads per pair and almost no issue time.
+//
+// Layout (same "transposed" formulation as pntf_field.h, 32-row tiles):
+//   * lane l = (j, h), j = l & 31 the pair, h = l >> 5; a 32-feature activation tile is one
+//     f32x16 per lane, register r holding feature row(r, h) = (r & 3) + 8 (r >> 2) + 4 h —
+//     exactly the C/D layout of v_mfma_f32_32x32x2_f32;
+//   * a layer's output tile is the next layer's B operand as is: instruction (kt, r) takes
+//     B = in[kt][r] (k-pair rows row(r, 0), row(r, 1)) and A = the weight column pair of the
+//     same rows, packed ("wide fragment order", pntf_pack_weights) so that one
+//     buffer_load_dwordx4 per lane fetches the A operands of 4 consecutive registers:
+//        P[(((ot·KT + kt)·4 + u)·64 + l)·4 + s] = M[32 ot + (l & 31)][32 kt + 8 u + 4 (l >> 5) + s]
+//   * the bias enters as one extra MFMA per out tile (A = the bias column on the h = 0 lanes,
+//     B = 1), and a residual as that MFMA's C operand, so neither costs VALU work;
+//   * activations live in two banks X[8], Y[8] (256 features, or 2 points x 128 features);
+//     saved σ10 tiles (4 KiB per 32-feature tile and point) go to a per-wave scratch slot.
+#include "pntf_field.h"
+
+namespace pntf {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+// feature row of register r in lane half h of a 32-row tile
+__device__ __forceinline__ constexpr int wrow(int r, int h) {
+  return (r & 3) + 8 * (r >> 2) + 4 * h;
+}
+
+// ---------------------------------------------------------------- scratch (saved σ10)
+struct WScratch {
+  Rsrc r;
+};
+__device__ __forceinline__ WScratch make_wscratch(float* p) {
+  return WScratch{make_rsrc(p, p ? WSCRATCH_FLOATS_PER_WAVE * 4 : 0)};
+}
+// tile t = 4 KiB: part q (registers 4q..4q+3) of all lanes is 1 KiB contiguous
+__device__ __forceinline__ void wstore(WScratch sc, int t, int lane, const f32x16& v) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 p{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+    __builtin_amdgcn_raw_buffer_store_b128(
+        __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, p), sc.r, lane * 16,
+        t * 4096 + q * 1024, AUX_NT);
+  }
+}
+__device__ __forceinline__ f32x16 wload(WScratch sc, int t, int lane) {
+  f32x16 v;
+#ifdef PNTF_ABL_NOLOAD    // diagnostics only (tests/diag ablations)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = 0.5f;
+  return v;
+#endif
+#ifdef PNTF_ABL_L2LOAD    // diagnostics only: same loads, from a 16 KiB L2-resident region
+  t &= 3;
+#endif
+#ifdef PNTF_ABL_UNUSED    // diagnostics only: the loads issue, their data is not used
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 p = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(sc.r, lane * 16, t * 4096 + q * 1024,
+                                                     AUX_LOAD));
+    asm volatile("" ::"v"(p));
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = 0.5f;
+  return v;
+#endif
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 p = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(sc.r, lane * 16, t * 4096 + q * 1024,
+                                                     AUX_LOAD));
+#pragma unroll
+    for (int s = 0; s < 4; ++s) v[4 * q + s] = p[s];
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------- weight stream heads
+constexpr int WF = (OFF_WIDE + OFF_FWD) * 4;   // byte base of the forward wide fragments
+constexpr int WB = (OFF_WIDE + OFF_BWD) * 4;   // ... of the transposed ones
+constexpr int WBC = (OFF_WIDE + W_OFF_BCOL) * 4;
+constexpr int WHW = (OFF_WIDE + W_OFF_G4W) * 4;
+constexpr int WG4B = (OFF_WIDE + W_OFF_G4B) * 4;
+
+// standard layer: step st = ot·KT + kt reads fragments (ot, kt, u = l)
+struct WHead {
+  int base;
+  __device__ int operator()(int j, int l) const { return base + (j * 4 + l) * 1024; }
+};
+// encoder[0] on Fourier features, k-tile outer: step st = kt·4 + ot (KT = 8)
+struct WE0Head {
+  __device__ int operator()(int j, int l) const {
+    return WF + OFF_E0 * 4 + ((((j % 4) * 8 + j / 4) * 4 + l) * 1024);
+  }
+};
+// reverse sweep head: generator[-2]^T (OT 8, KT 4)
+__device__ __forceinline__ WHead wbwd_head() { return WHead{WB + OFF_G3 * 4}; }
+// Fourier fold (encoder[0]^T, OT 8, KT 4): step st = (o·4 + kt)·2 + half reads out tile
+// o + 4·half (sin rows o, cos rows o + 4)
+struct WFoldHead {
+  __device__ int operator()(int j, int l) const {
+    const int o = j / 8, kt = (j / 2) % 4, half = j % 2;
+    return WB + OFF_E0 * 4 + ((((o + 4 * half) * 4 + kt) * 4 + l) * 1024);
+  }
+};
+
+// ---------------------------------------------------------------- generic wide layer
+// One Linear layer over OT out tiles x KT input tiles, NC columns (points) sharing the
+// weights; bank index of column c, tile t is c·OT + t (out) / c·KT + t (in).  Step st =
+// (ot, kt) runs 16·NC MFMAs on the 4 fragments of (ot, kt).  ly.init(ot, acc) starts out
+// tile ot (its bias MFMA, residual as C); ly.epi(ot, acc) finishes it — when L::DEFER, only
+// after the first step of the next out tile has issued its MFMAs (the last tile's at once).
+template <int OT, int KT, int NC, int SITE, int NLN, class L, class PreF, class NextF>
+__device__ __forceinline__ void wlayer(Ring& ring, Rsrc W, int wbase, const f32x16 (&in)[8],
+                                       int lane, L& ly, PreF pre, NextF naddr) {
+  static_assert(NC * KT <= 8 && NC * OT <= 8, "bank size");
+  constexpr int STEPS = OT * KT;
+  constexpr bool DEF = L::DEFER;          // epilogue deferred past the next tile's first step
+  f32x16 acc[DEF ? 2 : 1][NC];
+  run_steps<STEPS, 4, NLN, SITE>(
+      ring, W, lane * 16, WHead{wbase}, naddr, [&](auto st, const f32x4 (&a)[4]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int ot = S / KT, kt = S % KT, p = DEF ? (ot & 1) : 0;
+        if constexpr (S == 0) ly.start();
+        pre(st);
+        if constexpr (kt == 0) ly.init(ot, acc[p]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+              acc[p][c] = mfma32(a[u][s], in[c * KT + kt][4 * u + s], acc[p][c]);
+        if constexpr (DEF) {
+          if constexpr (kt == 0 && ot > 0) ly.epi(ot - 1, acc[p ^ 1]);
+          if constexpr (S == STEPS - 1) ly.epi(ot, acc[p]);
+        } else if constexpr (kt == KT - 1) {
+          ly.epi(ot, acc[p]);
+        }
+      });
+}
+
+// bias-column operands of a layer: fragment g holds out tiles 4g..4g+3 (lanes 0-31)
+template <int OT>
+struct BiasCols {
+  f32x4 v[(OT + 3) / 4];
+  __device__ __forceinline__ void load(Rsrc W, int lane, int plain_off) {
+#pragma unroll
+    for (int g = 0; g < (OT + 3) / 4; ++g)
+      v[g] = bload(W, lane * 16, WBC + ((plain_off / 128 + g) * 64) * 16);
+  }
+  __device__ __forceinline__ float operator()(int ot) const { return v[ot / 4][ot % 4]; }
+};
+
+// forward Linear + softplus10: out = sp(A·in + b (+ out if RES)); σ10 saved when SAVE
+template <int OT_, int KT_, int NC_, bool RES, bool SAVE>
+struct WFwdAct {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_;
+  static constexpr bool DEFER = true;
+  f32x16 (&out)[8];
+  WScratch sc;
+  int sc0, lane;
+  BiasCols<OT_> bc;   // loaded by the caller one layer ahead
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void init(int ot, f32x16 (&acc)[NC]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = mfma32(bc(ot), 1.f, RES ? out[c * OT + ot] : zero16());
+  }
+  __device__ __forceinline__ void epi(int ot, const f32x16 (&acc)[NC]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      f32x16 h, g;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        SpSig q = sp_sig(acc[c][r]);
+        h[r] = q.sp;
+        g[r] = q.sg;
+      }
+      out[c * OT + ot] = h;
+      if (SAVE) wstore(sc, sc0 + c * OT + ot, lane, g);
+    }
+  }
+};
+
+// forward Linear without activation (encoder[-1], :234)
+template <int OT_, int KT_, int NC_>
+struct WFwdLin {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_;
+  static constexpr bool DEFER = true;
+  f32x16 (&out)[8];
+  BiasCols<OT_> bc;
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void init(int ot, f32x16 (&acc)[NC]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = mfma32(bc(ot), 1.f, zero16());
+  }
+  __device__ __forceinline__ void epi(int ot, const f32x16 (&acc)[NC]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) out[c * OT + ot] = acc[c];
+  }
+};
+
+// reverse: out = (A^T·in (+ out if RES)) ⊙ σ tile (if MUL).  Both banks are full here, so
+// the σ tile is loaded into the out tile's own registers when the tile starts (its old value,
+// the residual, is dead once it is the accumulator's start), KT steps of MFMAs before the
+// epilogue multiplies it in place.  Not deferred (no second accumulator).  (Loading all of a
+// layer's σ tiles at its start measured slower.)
+template <int OT_, int KT_, int NC_, bool RES, bool MUL>
+struct WBwd {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_;
+  static constexpr bool DEFER = false;
+  f32x16 (&out)[8];
+  WScratch sc;
+  int mul0, lane;
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void init(int ot, f32x16 (&acc)[NC]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      acc[c] = RES ? out[c * OT + ot] : zero16();
+      if (MUL) out[c * OT + ot] = wload(sc, mul0 + c * OT + ot, lane);
+    }
+  }
+  __device__ __forceinline__ void epi(int ot, const f32x16 (&acc)[NC]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      out[c * OT + ot] = MUL ? acc[c] * out[c * OT + ot] : acc[c];
+  }
+};
+
+// ---------------------------------------------------------------- Fourier projections
+// q[c][r] = x_c · 2πB[:, 32 kt + row(r, h)] for the lane's 16 feature rows of Fourier tile
+// kt, both points; the B rows come from the pair's environment (io.Bw, dim x 128).
+template <int DIM>
+__device__ __forceinline__ void wfourier_q(const PairIO& io, int kt, int h, f32x16 (&q)[2]) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) q[c] = zero16();
+#pragma unroll
+  for (int d = 0; d < DIM; ++d)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      f32x4 b = ld4(io.Bw + d * H + 32 * kt + 8 * u + 4 * h);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) q[c][4 * u + s] = fmaf(io.x[c][d], TWO_PI * b[s], q[c][4 * u + s]);
+    }
+}
+
+// ---------------------------------------------------------------- forward pass
+// NN.out on 32 pairs.  GRAD: save σ tiles.  On entry the ring holds WE0Head; on return the
+// first PF steps of `after`.  Returns τ of the lane's pair (same in both lane halves).
+template <int DIM, bool GRAD, class AfterF>
+__device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& io,
+                                              f32x16 (&X)[8], f32x16 (&Y)[8], WScratch sc,
+                                              int compat, int lane, AfterF after) {
+  const int h = lane >> 5;
+  const float cm = compat ? 1.f : 0.f;
+
+  // ---- encoder[0] (:186-190, :227), k-tile outer: X[c·4 + ot] accumulate 4 out tiles x 2
+  // points; sin tiles (kt < 4) are computed at step (kt, 0), their cos partners (kt + 4)
+  // kept in Y[c·4 + kt] until then.
+  BiasCols<4> be0, a0bc;
+  BiasCols<8> gbc;
+  be0.load(W, lane, B_E0);
+  {
+    f32x16 q[2], sn[2];
+    wfourier_q<DIM>(io, 0, h, q);
+    run_steps<32, 4, 4, SITE_FWD_E0>(
+        ring, W, lane * 16, WE0Head{}, WHead{WF + OFF_EBLK * 4},
+        [&](auto st, const f32x4 (&a)[4]) {
+          constexpr int S = decltype(st)::value;
+          constexpr int kt = S / 4, ot = S % 4;
+          if constexpr (ot == 0 && kt < 4) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                float x0, x1;
+                sincos_fast(q[c][r], x0, x1);
+                sn[c][r] = x0;
+                Y[c * 4 + kt][r] = x1;
+              }
+          }
+          if constexpr (kt == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) X[c * 4 + ot] = mfma32(be0(ot), 1.f, zero16());
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+              for (int c = 0; c < 2; ++c) {
+                float b;
+                if constexpr (kt < 4) b = sn[c][4 * u + s];
+                else b = Y[c * 4 + kt - 4][4 * u + s];
+                X[c * 4 + ot] = mfma32(a[u][s], b, X[c * 4 + ot]);
+              }
+          // next sin/cos tile's projections, after this tile's MFMAs are issued
+          if constexpr (ot == 3 && kt < 3) wfourier_q<DIM>(io, kt + 1, h, q);
+          if constexpr (S == 16) a0bc.load(W, lane, B_EBLK);
+        });
+  }
+  // bias, softplus, σ (compat: the out_backgrad quirk :435-438 stores σ10(softplus(y)))
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    f32x16 s, g;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      SpSig v = sp_sig(X[t][r]);
+      s[r] = v.sp;
+      g[r] = fmaf(cm, __builtin_amdgcn_rcpf(2.f - v.sg) - v.sg, v.sg);
+    }
+    X[t] = s;
+    if (GRAD) wstore(sc, WT_E0 + t, lane, g);
+  }
+
+  // ---- encoder residual blocks (:228-232); X = h (2 points x 4 tiles).  Each layer's bias
+  // columns are fetched at the first step of the layer before it.
+  const int WE = WF + OFF_EBLK * 4;
+  {
+    WFwdAct<4, 4, 2, false, GRAD> a0{Y, sc, WT_EBLK, lane, {}};
+    WFwdAct<4, 4, 2, true, GRAD> b0{X, sc, WT_EBLK + 8, lane, {}};
+    WFwdAct<4, 4, 2, false, GRAD> a1{Y, sc, WT_EBLK + 16, lane, {}};
+    WFwdAct<4, 4, 2, true, GRAD> b1{X, sc, WT_EBLK + 24, lane, {}};
+    WFwdLin<4, 4, 2> e3{Y, {}};
+    a0.bc = a0bc;
+    wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WE, X, lane, a0,
+                                     at<0>([&] { b0.bc.load(W, lane, B_EBLK + 128); }),
+                                     WHead{WE + SZ_E * 4});
+    wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WE + SZ_E * 4, Y, lane, b0,
+                                     at<0>([&] { a1.bc.load(W, lane, B_EBLK + 256); }),
+                                     WHead{WE + 2 * SZ_E * 4});
+    wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
+                                     at<0>([&] { b1.bc.load(W, lane, B_EBLK + 384); }),
+                                     WHead{WE + 3 * SZ_E * 4});
+    wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
+                                     at<0>([&] { e3.bc.load(W, lane, B_E3); }),
+                                     WHead{WF + OFF_E3 * 4});
+    // ---- encoder[-1] (:234) -> Y (zs = Y[0..3], zg = Y[4..7])
+    wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WF + OFF_E3 * 4, X, lane, e3,
+                                     at<0>([&] { gbc.load(W, lane, B_GBLK); }),
+                                     WHead{WF + OFF_GBLK * 4});
+  }
+
+  // ---- symmetric smooth max / min merge (:236-244) -> X (u = [M | m], 8 tiles)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 s0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float zs = Y[t][r], zg = Y[4 + t][r];
+      float d = zs - zg;
+      float e = exp_neg10abs(d);
+      float cc = 0.1f * log1p_small(e);
+      X[t][r] = fmaxf(zs, zg) + cc;
+      X[4 + t][r] = fminf(zs, zg) - cc;
+      float rr = __builtin_amdgcn_rcpf(1.f + e);
+      s0[r] = (d >= 0.f) ? rr : e * rr;
+    }
+    if (GRAD) wstore(sc, WT_S0 + t, lane, s0);
+  }
+
+  // ---- generator residual blocks (:246-249); X = u (8 tiles); gbc carries the next
+  // layer's bias columns across the loop
+#pragma unroll 1
+  for (int i = 0; i < 3; ++i) {
+    const int wa = opaque(WF + (OFF_GBLK + (2 * i) * SZ_G) * 4);
+    const int wb = opaque(WF + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4);
+    const int wn = opaque(i < 2 ? WF + (OFF_GBLK + (2 * i + 2) * SZ_G) * 4 : WF + OFF_G3 * 4);
+    const int bo = opaque(B_GBLK + (2 * i) * 256);
+    const int bn = opaque(i < 2 ? B_GBLK + (2 * i + 2) * 256 : B_G3);
+    WFwdAct<8, 8, 1, false, GRAD> ga{Y, sc, WT_GBLK + 16 * i, lane, gbc};
+    WFwdAct<8, 8, 1, true, GRAD> gb{X, sc, WT_GBLK + 16 * i + 8, lane, {}};
+    wlayer<8, 8, 1, SITE_FWD_GEN, 4>(ring, W, wa, X, lane, ga,
+                                     at<0>([&] { gb.bc.load(W, lane, bo + 256); }),
+                                     WHead{wb});
+    wlayer<8, 8, 1, SITE_FWD_GEN, 4>(ring, W, wb, Y, lane, gb,
+                                     at<0>([&] { gbc.load(W, lane, bn); }), WHead{wn});
+  }
+  // ---- generator[-2] + act (:251-252) -> Y[0..3] (its bias columns: gbc's first 4 tiles)
+  {
+    WFwdAct<4, 8, 1, false, GRAD> g3{Y, sc, WT_G3, lane, {}};
+    g3.bc.v[0] = gbc.v[0];
+    wlayer<4, 8, 1, SITE_FWD_GEN, 4>(ring, W, WF + OFF_G3 * 4, X, lane, g3, NoPre{}, after);
+  }
+  // ---- head generator[-1] + sigmoid(0.1 y) (:254-255)
+  float part = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      f32x4 w = bload(W, lane * 16, WHW + ((4 * t + u) * 64) * 16);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) part = fmaf(w[s], Y[t][4 * u + s], part);
+    }
+  part += __shfl_xor(part, 32);
+  const float y4 = part + bload(W, 0, WG4B)[0];
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-0.144269504088896341f * y4));
+}
+
+// ---------------------------------------------------------------- reverse sweep
+// Exact reverse mode (or out_backgrad when the forward stored the quirk).  On entry the ring
+// holds wbwd_head(); on return the first PF steps of `after`.  ds/dg: dτ/dxs, dτ/dxg of the
+// lane's pair (same in both halves).
+template <int DIM, class AfterF>
+__device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& io, float tau,
+                                              f32x16 (&X)[8], f32x16 (&Y)[8], WScratch sc,
+                                              int lane, float (&ds)[DIM], float (&dg)[DIM],
+                                              AfterF after) {
+  const int h = lane >> 5;
+  // ---- head and generator[-2] (:592-613): Y[t] = d · g4w ⊙ σ10(y3)
+  const float dd = 0.1f * tau * (1.f - tau);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 s3 = wload(sc, WT_G3 + t, lane);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      f32x4 w = bload(W, lane * 16, WHW + ((4 * t + u) * 64) * 16);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) Y[t][4 * u + s] = (dd * w[s]) * s3[4 * u + s];
+    }
+  }
+  // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> X   (G3^T: 256 x 128, OT 8, KT 4)
+  {
+    WBwd<8, 4, 1, false, true> l{X, sc, WT_GBLK + 16 * 2 + 8, lane};
+    wlayer<8, 4, 1, SITE_BWD_GEN, 4>(ring, W, WB + OFF_G3 * 4, Y, lane, l, NoPre{},
+                                     WHead{WB + (OFF_GBLK + 5 * SZ_G) * 4});
+  }
+  // ---- generator blocks, reverse (:615-618): blocks 2 and 1 in a loop, block 0 peeled (its
+  // second layer multiplies by no σ and hands over to encoder[-1]^T)
+#pragma unroll 1
+  for (int i = 2; i >= 1; --i) {
+    const int wa = opaque(WB + (OFF_GBLK + (2 * i) * SZ_G) * 4);
+    const int wb = opaque(WB + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4);
+    const int wn = opaque(WB + (OFF_GBLK + (2 * i - 1) * SZ_G) * 4);
+    // da = (G1_i^T dr) ⊙ σ10(y1_i) -> Y
+    WBwd<8, 8, 1, false, true> lb{Y, sc, WT_GBLK + 16 * i, lane};
+    wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, wb, X, lane, lb, NoPre{}, WHead{wa});
+    // du = G_i^T da + dr, then ⊙ σ10(y2_{i-1})
+    WBwd<8, 8, 1, true, true> la{X, sc, WT_GBLK + 16 * (i - 1) + 8, lane};
+    wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, wa, Y, lane, la, NoPre{}, WHead{wn});
+  }
+  {
+    WBwd<8, 8, 1, false, true> lb{Y, sc, WT_GBLK, lane};
+    wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, WB + (OFF_GBLK + 1 * SZ_G) * 4, X, lane, lb,
+                                     NoPre{}, WHead{WB + OFF_GBLK * 4});
+    WBwd<8, 8, 1, true, false> la{X, sc, 0, lane};
+    wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, WB + OFF_GBLK * 4, Y, lane, la, NoPre{},
+                                     WHead{WB + OFF_E3 * 4});
+  }
+  // ---- merge Jacobian (:620-627): X[0..3] = dzs, X[4..7] = dzg
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 s0 = wload(sc, WT_S0 + t, lane);
+    f32x16 s1 = 1.f - s0;
+    f32x16 dM = X[t], dm = X[4 + t];
+    X[t] = s0 * dM + s1 * dm;
+    X[4 + t] = s1 * dM + s0 * dm;
+  }
+  // ---- encoder[-1]^T ⊙ σ10(y2 of encoder block 1), then the blocks, reverse (:629-636)
+  const int WE = WB + OFF_EBLK * 4;
+  {
+    WBwd<4, 4, 2, false, true> e3{Y, sc, WT_EBLK + 24, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
+                                     WHead{WE + 3 * SZ_E * 4});
+    WBwd<4, 4, 2, false, true> b1{X, sc, WT_EBLK + 16, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, NoPre{},
+                                     WHead{WE + 2 * SZ_E * 4});
+    WBwd<4, 4, 2, true, true> a1{Y, sc, WT_EBLK + 8, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
+                                     WHead{WE + 1 * SZ_E * 4});
+    WBwd<4, 4, 2, false, true> b0{X, sc, WT_EBLK, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, NoPre{},
+                                     WHead{WE});
+    WBwd<4, 4, 2, true, true> a0{Y, sc, WT_E0, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE, X, lane, a0, NoPre{}, WFoldHead{});
+  }
+
+  // ---- encoder[0]^T (256 x 128: OT 8, KT 4) fused with the Fourier Jacobian (:639-645).
+  // Feature tile o pairs sin rows (out tile o) with cos rows (out tile o + 4) of the same q;
+  // step (o, kt, half) accumulates half's out tile; after (o, 3, 1) the tile pair folds
+  //   dτ/dx_c += Σ_rows 2πB[:, f] (dφ_sin cos q_f - dφ_cos sin q_f)
+  float acc[2][DIM];
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) acc[0][d] = acc[1][d] = 0.f;
+  f32x16 ph[2][2];   // [sin | cos rows][point]
+  run_steps<32, 4, 4, SITE_FOLD>(
+      ring, W, lane * 16, WFoldHead{}, after, [&](auto st, const f32x4 (&a)[4]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int o = S / 8, kt = (S / 2) % 4, half = S % 2;
+        if constexpr (kt == 0) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) ph[half][c] = zero16();
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+              ph[half][c] = mfma32(a[u][s], Y[c * 4 + kt][4 * u + s], ph[half][c]);
+        if constexpr (kt == 3 && half == 1) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            f32x4 bw[DIM];
+#pragma unroll
+            for (int d = 0; d < DIM; ++d) bw[d] = TWO_PI * ld4(io.Bw + d * H + 32 * o + 8 * u + 4 * h);
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int s = 0; s < 4; ++s) {
+                float q = 0.f;
+#pragma unroll
+                for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], bw[d][s], q);
+                float sn, cs;
+                sincos_fast(q, sn, cs);
+                const int r = 4 * u + s;
+                float gg = ph[0][c][r] * cs - ph[1][c][r] * sn;
+#pragma unroll
+                for (int d = 0; d < DIM; ++d) acc[c][d] = fmaf(bw[d][s], gg, acc[c][d]);
+              }
+          }
+        }
+      });
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) {
+    ds[d] = acc[0][d] + __shfl_xor(acc[0][d], 32);
+    dg[d] = acc[1][d] + __shfl_xor(acc[1][d], 32);
+  }
+}
+
+// ---------------------------------------------------------------- kernel
+template <int DIM, int KIND>
+__global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
+  constexpr bool GRAD = KIND != K_TAU && KIND != K_TRAVEL;
+  const int lane = threadIdx.x & 63;
+  const int slot = blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nslots = gridDim.x * WAVES;
+  // tile indices are wave-uniform 32-bit values (kept in SGPRs; n < 2^36 pairs)
+  const int ntiles = (int)((a.n + WTILE - 1) / WTILE);
+  const WScratch sc =
+      make_wscratch(GRAD ? a.ws + (int64_t)slot * WSCRATCH_FLOATS_PER_WAVE : nullptr);
+  const Rsrc W = make_rsrc(a.P, PACKED_TOTAL * 4);
+  Ring ring;
+  ring_fill<4>(ring, W, lane * 16, WE0Head{});
+  for (int tile = slot; tile < ntiles; tile += nslots) {
+    f32x16 X[8], Y[8];
+    // the pair column, re-derived per tile from the lane·16 byte offset every load keeps
+    // live (through an opaque copy, so it is not hoisted): a separate loop-invariant copy was
+    // the one value that spilled
+    int v16 = lane * 16;
+    asm volatile("" : "+v"(v16));
+    const int64_t pair = (int64_t)(tile * WTILE + ((v16 >> 4) & 31));
+    PairIO io;
+    const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
+    float tau;
+    if constexpr (GRAD)
+      tau = wide_forward<DIM, true>(ring, W, io, X, Y, sc, a.compat, lane, wbwd_head());
+    else
+      tau = wide_forward<DIM, false>(ring, W, io, X, Y, sc, a.compat, lane, WE0Head{});
+    float ds[DIM], dg[DIM];
+    if constexpr (GRAD) {
+      drain_stores();
+      wide_backward<DIM>(ring, W, io, tau, X, Y, sc, lane, ds, dg, WE0Head{});
+    }
+    const bool store = lane < 32 && pair < a.n;
+    store_field<DIM, KIND>(a, pair, ok, store, tau, io, ds, dg);
+  }
+}
+
+#if defined(PNTF_UTIL)
+// ---------------------------------------------------------------- wide weight packing
+// dst[(((ot·KT + kt)·4 + u)·64 + l)·4 + s] = M[32 ot + (l & 31)][32 kt + 8 u + 4 (l >> 5) + s]
+// with M = src (rows x cols, row stride ld) or M = src^T (trans).
+__global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int cols, int ld,
+                                 int trans, float* __restrict__ dst) {
+  int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= (int64_t)rows * cols) return;
+  int s = o & 3;
+  int l = (o >> 2) & 63;
+  int u = (o >> 8) & 3;
+  int64_t rest = o >> 10;
+  int KT = cols / 32;
+  int kt = rest % KT;
+  int ot = rest / KT;
+  int n = 32 * ot + (l & 31);
+  int k = 32 * kt + 8 * u + 4 * (l >> 5) + s;
+  dst[o] = trans ? src[(int64_t)k * ld + n] : src[(int64_t)n * ld + k];
+}
+
+// bias columns, head vector and head bias of the wide region, from the plain bias block
+__global__ void pack_wide_aux_kernel(const float* __restrict__ plain, float* __restrict__ wide) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int NB = W_SZ_BCOL, NH = W_SZ_G4W;
+  if (o < NB) {   // bias columns: fragment g, lane l, element s
+    int s = o & 3, l = (o >> 2) & 63, g = o >> 8;
+    wide[W_OFF_BCOL + o] = l < 32 ? plain[128 * g + 32 * s + l] : 0.f;
+  } else if (o < NB + NH) {   // head vector: fragment (4t + u)
+    int p = o - NB;
+    int s = p & 3, l = (p >> 2) & 63, f = p >> 8;
+    int t = f / 4, u = f % 4;
+    wide[W_OFF_G4W + p] = plain[B_G4W + 32 * t + 8 * u + 4 * (l >> 5) + s];
+  } else if (o < NB + NH + 4) {
+    wide[W_OFF_G4B + (o - NB - NH)] = plain[B_G4B + (o - NB - NH)];
+  }
+}
+#endif  // PNTF_UTIL
+
+}  // namespace pntf

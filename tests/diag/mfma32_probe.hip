@@ -106,6 +106,52 @@ void vrun(float* out, long long* cyc, int grid) {
   printf("32x32x2 + %d %s per MFMA  cycles/MFMA = %.2f\n", NV, VK ? "exp" : "fma", m / (iters * 4.0));
 }
 
+// ds_read_b128 beside 32x32x2: NR LDS fragment reads per 4 MFMAs (operands consumed)
+template <int NR>
+__global__ __launch_bounds__(256, 1) void dprobe(float* out, long long* cyc, int iters) {
+  __shared__ float lds[16 * 256];
+  typedef __attribute__((address_space(3))) f32x4 l4;
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < 16 * 256; i += 256) lds[i] = 0.001f * i;
+  __syncthreads();
+  f32x16 acc[2] = {};
+  float b = 1.0f + threadIdx.x * 1e-4f;
+  f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0;
+  long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    l4* L = (l4*)lds;
+    f32x4 n0 = r0, n1 = r1;
+    if (NR >= 1) n0 = L[((it * 2) & 15) * 64 + lane];
+    if (NR >= 2) n1 = L[((it * 2 + 1) & 15) * 64 + lane];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      acc[m & 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(NR ? (m < 2 ? r0[m] : r1[m]) : b, b, acc[m & 1], 0, 0, 0);
+    r0 = n0;
+    r1 = n1;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  long long t1 = __builtin_amdgcn_s_memtime();
+  float sm = r0[0] + r1[1];
+  for (int i = 0; i < 16; ++i) sm += acc[0][i] + acc[1][i];
+  out[blockIdx.x * 256 + threadIdx.x] = sm;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int NR>
+void drun(float* out, long long* cyc, int grid) {
+  const int iters = 4000;
+  for (int rep = 0; rep < 2; ++rep) {
+    dprobe<NR><<<grid, 256>>>(out, cyc, iters);
+    (void)hipDeviceSynchronize();
+  }
+  long long h[1024];
+  (void)hipMemcpy(h, cyc, grid * sizeof(long long), hipMemcpyDeviceToHost);
+  double m = 0;
+  for (int i = 0; i < grid; ++i) m += h[i];
+  m /= grid;
+  printf("32x32x2 + %d ds_read_b128 per 4 MFMA  cycles/MFMA = %.2f\n", NR, m / (iters * 4.0));
+}
+
 int main() {
   float *w, *out;
   long long* cyc;
@@ -129,5 +175,8 @@ int main() {
   vrun<2, 1>(out, cyc, grid);
   vrun<4, 1>(out, cyc, grid);
   vrun<6, 1>(out, cyc, grid);
+  drun<0>(out, cyc, grid);
+  drun<1>(out, cyc, grid);
+  drun<2>(out, cyc, grid);
   return 0;
 }

@@ -1,14 +1,22 @@
 // Perf-variant builds of the τ+∇τ kernel (dim 3, exact mode) under other weight-stream
 // parameters (-DPNTF_PF_STEPS, -DPNTF_NO1).  Diagnostics only; built by
 // tests/diag/build_perf.sh into tests/diag/libperf_<name>.so and timed by perf_variants.py.
+#ifdef PERF_WIDE
+#include "pntf_wide.h"
+#else
 #include "pntf_field.h"
+#endif
 
 extern "C" int perf_tau_grad(int grid, const float* P, const float* xp, int64_t n,
                              const float* Btab, float* tau, float* dtau, float* ws,
                              hipStream_t stream) {
   using namespace pntf;
   FieldArgs a{P, xp, Btab, nullptr, n, 1, 0, tau, dtau, ws};
+#ifdef PERF_WIDE
+  hipLaunchKernelGGL((wide_field_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(256), 0, stream, a);
+#else
   hipLaunchKernelGGL((field_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(256), 0, stream, a);
+#endif
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -60,8 +60,8 @@ def main(names):
     t_ref, d_ref = ops.tau_grad(packed, xp, B[0], dim=3)
     torch.cuda.synchronize()
     grid = torch.cuda.get_device_properties(0).multi_processor_count
-    slot = 192 * 256 * 4
-    ws = torch.empty(grid * 8 * slot, dtype=torch.uint8, device=dev)
+    slot = 96 * 1024 * 4            # the larger (wide) slot
+    ws = torch.empty(grid * 4 * slot, dtype=torch.uint8, device=dev)
     V = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
     stream = torch.cuda.current_stream().cuda_stream
     for name in names:

@@ -45,9 +45,12 @@ def test_pure_queries_without_gpu(lib):
     lib.pntf_abi_version.restype = ctypes.c_int
     assert lib.pntf_abi_version() == 1
     lib.pntf_packed_floats.restype = ctypes.c_size_t
-    # forward + transposed fragments of 13 matrices + biases/head
+    # forward + transposed fragments of 13 matrices + biases/head (16x16 blob), then the same
+    # matrices in wide fragment order + 19 bias-column fragments + 16 head fragments + head bias
     mats = 128 * 256 + 4 * 128 * 128 + 128 * 128 + 6 * 256 * 256 + 128 * 256
-    assert lib.pntf_packed_floats() == 2 * mats + 128 + 4 * 128 + 128 + 6 * 256 + 128 + 128 + 4
+    plain = 128 + 4 * 128 + 128 + 6 * 256 + 128 + 128 + 4
+    wide = 2 * mats + 19 * 256 + 16 * 256 + 4
+    assert lib.pntf_packed_floats() == 2 * mats + plain + wide
     lib.pntf_status_string.restype = ctypes.c_char_p
     assert lib.pntf_status_string(1) == b"invalid argument"
 
@@ -140,6 +143,31 @@ def test_pack_layout_is_a_permutation_and_feeds_mfma_fragments():
                                   W.T[16 * ot + i, 16 * kt + 4 * g:16 * kt + 4 * g + 4])
 
 
+def _pack_wide_numpy(W):
+    """Restatement of pack_wide_kernel (pntf_wide.h): element o of the wide fragment stream."""
+    rows, cols = W.shape
+    o = np.arange(rows * cols)
+    s, lane, u, rest = o & 3, (o >> 2) & 63, (o >> 8) & 3, o >> 10
+    KT = cols // 32
+    kt, ot = rest % KT, rest // KT
+    return W[32 * ot + (lane & 31), 32 * kt + 8 * u + 4 * (lane >> 5) + s]
+
+
+def test_wide_pack_layout_feeds_32x32x2_fragments():
+    """Wide fragment (ot, kt, u), lane (i, h), element s holds W[32 ot + i][32 kt + 8u + 4h + s]:
+    the A operand of the MFMA that takes register r = 4u + s of input tile kt as B, whose
+    k rows are row(r, h) = (r & 3) + 8 (r >> 2) + 4 h (v_mfma_f32_32x32x2_f32 C/D layout)."""
+    rng = np.random.default_rng(1)
+    W = rng.standard_normal((256, 128)).astype(np.float32)
+    P = _pack_wide_numpy(W)
+    assert np.array_equal(np.sort(P), np.sort(W.ravel()))
+    frag = P.reshape(8, 4, 4, 64, 4)          # (ot, kt, u, lane, s)
+    row = lambda r, h: (r & 3) + 8 * (r >> 2) + 4 * h   # noqa: E731
+    for ot, kt, r, i, h in [(0, 0, 0, 0, 0), (5, 3, 13, 17, 1), (7, 1, 6, 31, 0)]:
+        u, s = r // 4, r % 4
+        assert frag[ot, kt, u, 32 * h + i, s] == W[32 * ot + i, 32 * kt + row(r, h)]
+
+
 def test_synth_is_deterministic():
     np.testing.assert_array_equal(synth.make_pairs(100, 3, 2), synth.make_pairs(100, 3, 2))
     x = synth.make_pairs(5000, 3, 2)
@@ -159,7 +187,7 @@ def test_field_ex_validates_kind_and_schedule_without_gpu():
     assert b"schedule" in L.pntf_last_error()
     # empty batch: valid for every kind and schedule, nothing launched
     for kind in range(5):
-        for sched in range(3):
+        for sched in range(4):
             assert L.pntf_field_ex(kind, None, 3, None, 0, None, None, 1, 0, None, None, None, 0,
                                    sched, None) == 0
 

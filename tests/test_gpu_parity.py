@@ -51,10 +51,11 @@ def packed(W, dev):
     return ops.pack_weights(params)
 
 
-@pytest.fixture(params=["wave_tile", "split_tile"])
+@pytest.fixture(params=["wave_tile", "split_tile", "wide_tile"])
 def field_schedule(request):
-    """Run a field test with one wave per tile and with split tiles (pntf_split.h); the
-    schedule is passed per call (pntf_field_ex), no library state changes."""
+    """Run a field test with one wave per 16-pair tile, with split tiles (pntf_split.h) and
+    with one wave per 32-pair tile (pntf_wide.h); the schedule is passed per call
+    (pntf_field_ex), no library state changes."""
     return request.param
 
 
@@ -330,10 +331,15 @@ def test_residual_grad_agrees_with_reverse_sweep(packed, dev):
     Bt = T(synth.make_B_table(10, 3), dev)
     env = T(synth.make_env_ids(n, 10), dev, torch.int32)
     out = ops.eikonal_residual(packed, xp, Bt, env, 3, want=("tau", "dtau", "ltau"))
-    t, d = ops.tau_grad(packed, xp, Bt, env, dim=3)
+    # the 16-pair τ+∇τ kernel runs the same forward MFMA sequence: τ bit-identical
+    t, d = ops.tau_grad(packed, xp, Bt, env, dim=3, schedule="wave_tile")
     assert torch.equal(out["tau"], t)
     assert torch.isfinite(out["ltau"]).all()
     close(out["dtau"].cpu().numpy(), d.cpu().numpy(), tol=1e-5)
+    # the 32-pair (wide) kernel sums in another order: fp32-rounding agreement
+    tw, dw = ops.tau_grad(packed, xp, Bt, env, dim=3, schedule="wide_tile")
+    close(tw.cpu().numpy(), t.cpu().numpy(), tol=1e-6)
+    close(out["dtau"].cpu().numpy(), dw.cpu().numpy(), tol=1e-5)
 
 
 def test_device_sum_deterministic(dev):

@@ -1,0 +1,258 @@
+"""Parity at trained weights.
+
+tests/golden/make_w2_goldens.py trained both reference models for 400 steps (the reference's
+own Model.Loss + loss.backward() + AdamW on an analytic sphere speed field), saved them with
+the reference's own Model.save (ckpt_w2_d3.pt, ckpt_w2_d6.pt), reloaded them with the
+reference's Model.load, and recorded the reference's outputs.  Here:
+  * CPU: the checkpoints load with torch.load(weights_only=True) and the fp64 oracle matches
+    the reference's outputs at those weights (τ, ∇τ, out_grad, out_backgrad, epilogues, Taylor
+    mode + Loss, planners);
+  * GPU: the drop-in Model.load reads the reference-written files (the arm one restores
+    B_state_dict) and the HIP path matches the same goldens (tolerances of
+    test_gpu_parity.close), the planners reproduce the reference's batch-1 loops, and the
+    C5 workload (1024 arm queries, ≤199 steps) matches the reference's 1024 batch-1 loops.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import GOLDEN, load, max_rel, rel_l2, weight_checksum
+from oracle import pntf_oracle as O
+from pntf import synth
+
+TOL = 1e-5          # fp64 oracle vs fp32 reference (as test_oracle_golden.py)
+CKPT = {3: os.path.join(GOLDEN, "ckpt_w2_d3.pt"), 6: os.path.join(GOLDEN, "ckpt_w2_d6.pt")}
+
+
+def ckpt(dim):
+    return torch.load(CKPT[dim], map_location="cpu", weights_only=True)
+
+
+def w2(dim):
+    sd = ckpt(dim)["model_state_dict"]
+    return {k: v.numpy().astype(np.float32) for k, v in sd.items()}
+
+
+# ------------------------------------------------------------------ CPU
+@pytest.mark.parametrize("dim", [3, 6])
+def test_reference_checkpoint_format(dim):
+    """Model.save's dict (multi :1143-1152, arm :1139-1148), loadable weights-only."""
+    c = ckpt(dim)
+    assert set(c) == {"epoch", "model_state_dict", "optimizer_state_dict", "B_state_dict",
+                      "train_loss", "val_loss"}
+    assert list(c["model_state_dict"]) == synth.state_dict_keys()
+    B = c["B_state_dict"]
+    assert tuple(B.shape) == ((3, 128) if dim == 3 else (128, 6))
+    name = "fwd_grad_w2_d3.npz" if dim == 3 else "fwd_grad_w2_d6.npz"
+    np.testing.assert_array_equal(weight_checksum(w2(dim)), load(name)["weight_checksum"])
+    # trained: far from the seeded start, and softplus's identity branch is exercised
+    W0 = synth.make_weights(0)
+    assert max(float(np.abs(w2(dim)[k] - W0[k]).max()) for k in W0) > 0.1
+    assert float(load(name)["softplus_saturation"]) > 0.01
+
+
+def test_w2_oracle_tau_grad_and_epilogues():
+    W = w2(3)
+    f = load("fwd_grad_w2_d3.npz")
+    t, d = O.tau_grad(W, f["xp"], f["B"])
+    assert rel_l2(t, f["tau"]) < TOL
+    assert rel_l2(d, f["dtau"]) < TOL and rel_l2(d, f["dtau_fwdmode"]) < TOL
+    tc, dc = O.tau_grad(W, f["xp"], f["B"], compat=True)
+    assert rel_l2(tc, f["tau_backgrad"]) < TOL and rel_l2(dc, f["dtau_backgrad"]) < TOL
+    assert rel_l2(O.path_velocity(f["xp"], tc, dc), f["gradient"]) < TOL
+    assert rel_l2(O.speed(f["xp"], t, d), f["speed"]) < TOL
+    assert rel_l2(O.travel_time(f["xp"], t), f["travel_time"]) < TOL
+
+
+def test_w2_oracle_laplace_and_loss():
+    W = w2(3)
+    f = load("loss_w2_d3.npz")
+    E, n, _ = f["pts"].shape
+    env = np.repeat(np.arange(E), n)
+    tau, dtau, ltau, diff = O.eikonal_residual(W, f["pts"].reshape(-1, 6),
+                                               f["yobs"].reshape(-1, 2), f["B_table"], env,
+                                               gamma=float(f["gamma"]))
+    assert rel_l2(tau, f["tau"].reshape(-1, 1)) < TOL
+    assert rel_l2(dtau, f["dtau"].reshape(-1, 6)) < TOL
+    assert rel_l2(ltau, f["ltau"].reshape(-1, 6)) < 1e-4
+    assert rel_l2(diff, f["diff"].reshape(-1)) < 1e-4
+    assert abs(O.loss_n(diff, f["B_table"], E, n) - float(f["loss_n"])) < 1e-5
+
+
+def test_w2_oracle_arm():
+    W = w2(6)
+    a = load("fwd_grad_w2_d6.npz")
+    t, d = O.tau_grad(W, a["xp"], a["B"].T, dim=6)
+    assert rel_l2(t, a["tau"]) < TOL and rel_l2(d, a["dtau"]) < TOL
+    v = O.path_velocity(a["xp"][:16], t[:16], d[:16], dim=6)
+    assert max_rel(v, a["gradient16"], 1e-3) < 1e-4
+    f = load("loss_w2_d6.npz")
+    tau, dtau, ltau, diff = O.eikonal_residual_arm(W, f["pts"], f["yobs"], f["B"].T, dim=6,
+                                                   gamma=float(f["gamma"]))
+    assert rel_l2(dtau, f["dtau"]) < TOL and rel_l2(ltau, f["ltau"]) < 1e-4
+    assert rel_l2(diff, f["diff"]) < 1e-4
+
+
+def test_w2_oracle_planners():
+    p = load("plan_gib_w2.npz")
+    path, steps = O.plan(w2(3), p["starts"], p["B"], step=0.03, tol=0.06, max_iter=500,
+                         compat=True)
+    np.testing.assert_array_equal(steps, p["iters"])
+    assert np.abs(path - p["paths"]).max() < 1e-4
+    a = load("plan_arm_w2.npz")
+    path, steps = O.plan(w2(6), a["starts"], a["B"].T, dim=6, step=0.015, tol=0.03,
+                         max_iter=300, compat=False)
+    np.testing.assert_array_equal(steps, a["iters"])
+    assert np.abs(path - a["paths"]).max() < 1e-4
+
+
+def test_w2_oracle_c5_sample():
+    """The first 64 of the 1024 C5 queries through the fp64 oracle planner vs the reference's
+    batch-1 loops (the GPU test covers all 1024)."""
+    c = load("plan_c5_w2.npz")
+    q = 64
+    path, steps = O.plan(w2(6), c["xq"][:q], ckpt(6)["B_state_dict"].numpy().T, dim=6,
+                         step=0.015, tol=0.03, max_iter=int(c["max_iter"]), compat=False)
+    np.testing.assert_array_equal(steps, c["iters"][:q])
+    assert np.abs(path[np.arange(q), steps] - c["final"][:q]).max() < 1e-4
+    assert np.abs(path[:16] - c["paths16"]).max() < 1e-4
+
+
+# ------------------------------------------------------------------ GPU
+def _T(a, dev, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device=dev, dtype=dtype)
+
+
+@pytest.fixture(scope="module")
+def multi():
+    from models import model_res_sigmoid_multi as md
+    m = md.Model(".", ".", 3, 2, device="cuda:0")
+    m.load(CKPT[3])                       # drop-in loader on the reference-written file
+    return m
+
+
+@pytest.fixture(scope="module")
+def arm():
+    from models import model_res_sigmoid as ma
+    m = ma.Model(".", ".", 6, device="cuda:0")
+    m.load(CKPT[6])                       # restores B_state_dict
+    return m
+
+
+@pytest.mark.gpu
+def test_w2_drop_in_load_and_fields(multi):
+    from test_gpu_parity import close
+    dev = torch.device("cuda:0")
+    f = load("fwd_grad_w2_d3.npz")
+    xp, B = _T(f["xp"], dev), _T(f["B"], dev)
+    tau, coords = multi.network.out(xp, B)
+    close(tau.detach().cpu().numpy(), f["tau"])
+    close(multi.gradient(tau, coords).cpu().numpy(), f["dtau"])
+    _, d1, _ = multi.network.out_grad(xp, B)
+    close(d1.cpu().numpy(), f["dtau_fwdmode"])
+    t2, d2, _ = multi.network.out_backgrad(xp, B)
+    close(t2.cpu().numpy(), f["tau_backgrad"])
+    close(d2.cpu().numpy(), f["dtau_backgrad"])
+    close(multi.Gradient(xp.clone(), B).cpu().numpy(), f["gradient"])
+    multi.B = B
+    close(multi.Speed(xp).cpu().numpy(), f["speed"])
+    close(multi.TravelTimes(xp).cpu().numpy(), f["travel_time"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile", "wide_tile"])
+def test_w2_field_schedules(multi, schedule):
+    from pntf import ops
+    from test_gpu_parity import close
+    dev = torch.device("cuda:0")
+    f = load("fwd_grad_w2_d3.npz")
+    t, d = ops.tau_grad(multi.network.packed(), _T(f["xp"], dev), _T(f["B"], dev), dim=3,
+                        schedule=schedule)
+    close(t.cpu().numpy(), f["tau"][:, 0])
+    close(d.cpu().numpy(), f["dtau"])
+
+
+@pytest.mark.gpu
+def test_w2_laplace_and_loss(multi, arm):
+    from test_gpu_parity import close
+    dev = torch.device("cuda:0")
+    f = load("loss_w2_d3.npz")
+    pts, Bt = _T(f["pts"], dev), _T(f["B_table"], dev)
+    tau, dtau, ltau, _ = multi.network.out_laplace(pts, Bt)
+    close(tau.cpu().numpy(), f["tau"])
+    close(dtau.cpu().numpy(), f["dtau"])
+    close(ltau.cpu().numpy(), f["ltau"])
+    with torch.no_grad():
+        _, loss_n, diff = multi.Loss(pts, _T(f["yobs"], dev), Bt, 1.0, float(f["gamma"]))
+    close(diff.cpu().numpy(), f["diff"])
+    assert abs(float(loss_n) - float(f["loss_n"])) < 1e-4 * abs(float(f["loss_n"]))
+    g = load("loss_w2_d6.npz")
+    pts = _T(g["pts"], dev)
+    tau, dtau, ltau, _ = arm.network.out_laplace(pts)
+    close(dtau.cpu().numpy(), g["dtau"])
+    close(ltau.cpu().numpy(), g["ltau"])
+    with torch.no_grad():
+        _, _, diff = arm.Loss(pts, _T(g["yobs"], dev), 1.0, float(g["gamma"]))
+    close(diff.cpu().numpy(), g["diff"])
+
+
+@pytest.mark.gpu
+def test_w2_arm_fields(arm):
+    from test_gpu_parity import close
+    dev = torch.device("cuda:0")
+    a = load("fwd_grad_w2_d6.npz")
+    np.testing.assert_array_equal(arm.B.cpu().numpy(), a["B"])      # B_state_dict restored
+    xp = _T(a["xp"], dev)
+    tau, coords = arm.network.out(xp)
+    close(tau.detach().cpu().numpy(), a["tau"])
+    close(arm.gradient(tau, coords).cpu().numpy(), a["dtau"])
+    g = torch.cat([arm.Gradient(xp[i:i + 1].clone()) for i in range(16)])
+    close(g.cpu().numpy(), a["gradient16"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile"])
+def test_w2_planners_vs_reference(multi, arm, schedule):
+    from pntf import ops
+    dev = torch.device("cuda:0")
+    p = load("plan_gib_w2.npz")
+    path, steps = ops.plan(multi.network.packed(), _T(p["starts"], dev), _T(p["B"], dev),
+                           dim=3, step=0.03, tol=0.06, max_iter=500,
+                           mode=ops.GRAD_BACKGRAD_COMPAT, schedule=schedule)
+    np.testing.assert_array_equal(steps.cpu().numpy(), p["iters"])
+    assert np.abs(path.cpu().numpy() - p["paths"]).max() < 1e-3
+    a = load("plan_arm_w2.npz")
+    path, steps = ops.plan(arm.network.packed(), _T(a["starts"], dev), _T(a["B"].T, dev),
+                           dim=6, step=0.015, tol=0.03, max_iter=300, mode=ops.GRAD_EXACT,
+                           schedule=schedule)
+    np.testing.assert_array_equal(steps.cpu().numpy(), a["iters"])
+    assert np.abs(path.cpu().numpy() - a["paths"]).max() < 1e-3
+
+
+@pytest.mark.gpu
+def test_w2_c5_1024_queries_vs_reference(arm):
+    """C5 at full size: 1024 arm queries, ≤199 steps, per-query freeze (Model.Plan, the
+    bench's planner call) vs 1024 independent reference batch-1 loops (test/arm_plan.py) at
+    trained weights, where plans run 100-200 steps.  Both sides are fp32 and differ in
+    summation order, so a query whose distance crosses tol within rounding of the stop test
+    may stop a step or so apart: at least 99 % of the iteration counts must be identical (any
+    other within 3 steps, with its own stop taken legitimately at |xg - xs| <= tol), final
+    states of identical-count queries and the 16 stored full paths within 1e-3."""
+    dev = torch.device("cuda:0")
+    c = load("plan_c5_w2.npz")
+    tol = float(c["tol"])
+    path, steps = arm.Plan(_T(c["xq"], dev), step=0.015, tol=tol, max_iter=int(c["max_iter"]))
+    path, steps = path.cpu().numpy(), steps.cpu().numpy()
+    ref = c["iters"]
+    same = steps == ref
+    assert same.mean() >= 0.99, (int((~same).sum()), np.nonzero(~same)[0][:10].tolist())
+    assert np.abs(steps - ref).max() <= 3
+    q = np.arange(len(steps))
+    fin = path[q, steps]
+    dist = np.linalg.norm(fin[:, 6:] - fin[:, :6], axis=1)
+    assert np.all((dist <= tol) | (steps > int(c["max_iter"])))
+    assert np.abs(fin[same] - c["final"][same]).max() < 1e-3
+    s16 = same[:16]
+    assert np.abs(path[:16][s16] - c["paths16"][s16]).max() < 1e-3

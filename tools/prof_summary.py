@@ -1,6 +1,6 @@
 """Summarise rocprofv3 outputs (gpurun_out/) into committed profiles/ files.
 
-    python tools/prof_summary.py --tag r01 --pairs 1048576 [--kernel field_kernel<3, 1>]
+    python tools/prof_summary.py --tag r02 --pairs 1048576 [--kernel wide_field_kernel<3, 1>]
 
 Reads gpurun_out/prof_stats/run_kernel_stats.csv (kernel-trace --stats) and the separate
 PMC passes gpurun_out/pmc_{fetch,write,mfma}/run_counter_collection.csv, applies the gfx950
@@ -34,8 +34,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--pairs", type=int, default=1 << 20)
-    ap.add_argument("--kernel", default="field_kernel<3, 1>")
-    ap.add_argument("--unit", default="field_d3_k1", help="build unit of --kernel")
+    ap.add_argument("--kernel", default="wide_field_kernel<3, 1>")
+    ap.add_argument("--unit", default="wide_d3_k1", help="build unit of --kernel")
     a = ap.parse_args()
     import sys
     sys.path.insert(0, os.path.join(ROOT, "p-ntfields_amd"))

@@ -49,11 +49,15 @@ typedef enum {
  *   SPLIT_TILE  the 4 waves of a workgroup share a 16-pair tile (pntf_split.h; latency);
  *   WIDE_TILE   one wave per 32-pair tile, v_mfma_f32_32x32x2_f32 (pntf_wide.h; throughput,
  *               field entry points only — the planner treats it as WAVE_TILE);
- *   AUTO        split while ceil(n/16) <= 2 x the CU count, wide above. */
+ *   QUAD_TILE   the 4 waves of a workgroup share a 4-pair tile, v_mfma_f32_4x4x1_16b_f32
+ *               (pntf_quad.h; lowest latency per planner step, no workspace needed);
+ *   AUTO        quad while ceil(n/4) <= the CU count, split while ceil(n/16) <= 2 x the CU
+ *               count, wide above. */
 #define PNTF_SCHED_AUTO 0
 #define PNTF_SCHED_WAVE_TILE 1
 #define PNTF_SCHED_SPLIT_TILE 2
 #define PNTF_SCHED_WIDE_TILE 3
+#define PNTF_SCHED_QUAD_TILE 4
 
 int pntf_abi_version(void);
 const char* pntf_status_string(int status);

@@ -20,6 +20,10 @@ template <int DIM>
 __global__ void plan_kernel(PlanArgs a);
 template <int DIM>
 __global__ void plan_split_kernel(PlanArgs a);
+template <int DIM, int KIND>
+__global__ void field_quad_kernel(FieldArgs a);
+template <int DIM>
+__global__ void plan_quad_kernel(PlanArgs a);
 template <int DIM>
 __global__ void residual_kernel(ResidualArgs a);
 __global__ void sum_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ out);
@@ -29,6 +33,9 @@ __global__ void copy_kernel(const float* __restrict__ src, int n, float* __restr
 __global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int cols, int ld,
                                  int trans, float* __restrict__ dst);
 __global__ void pack_wide_aux_kernel(const float* __restrict__ plain, float* __restrict__ wide);
+__global__ void pack_quad_kernel(const float* __restrict__ src, int rows, int cols, int dir,
+                                 float* __restrict__ dst);
+__global__ void pack_quad_aux_kernel(const float* __restrict__ plain, float* __restrict__ quad);
 }  // namespace pntf
 
 using namespace pntf;
@@ -84,10 +91,26 @@ static int64_t wide_grid_for(int64_t n) {
   return wgs < cap ? (wgs < 1 ? 1 : wgs) : cap;
 }
 
+// quad grid (pntf_quad.h): 4-pair tiles, one 4-wave workgroup per tile, at most one per CU
+static int64_t quad_grid_for(int64_t n) {
+  int64_t ntiles = (n + 3) / 4;
+  int64_t cap = (int64_t)num_cus();
+  return ntiles < cap ? (ntiles < 1 ? 1 : ntiles) : cap;
+}
+
+// Quad tiles while every tile gets a CU of its own: a planner step of a 4-pair tile is bound
+// by the CU's weight stream, not by its MFMAs.
+static bool use_quad(int64_t n, int schedule) {
+  if (schedule == PNTF_SCHED_QUAD_TILE) return true;
+  if (schedule != PNTF_SCHED_AUTO) return false;
+  return (n + 3) / 4 <= (int64_t)num_cus();
+}
+
 static int grid_with_ws(int64_t n, size_t ws_bytes, int64_t* grid, bool split = false,
                         bool wide = false) {
   int64_t g = split ? split_grid_for(n) : wide ? wide_grid_for(n) : grid_for(n);
-  int64_t fit = (int64_t)(ws_bytes / ((wide ? WSLOT_BYTES : SLOT_BYTES) * WAVES));
+  int64_t fit = (int64_t)(ws_bytes / ((wide ? WSLOT_BYTES : SLOT_BYTES) *
+                                      (split ? SPLIT_WAVES : WAVES)));
   if (fit < 1) return fail(PNTF_ERR_WORKSPACE, "workspace too small (%s)", "need >= 4 slots");
   *grid = g < fit ? g : fit;
   return PNTF_OK;
@@ -108,7 +131,7 @@ static int g_field_schedule = PNTF_SCHED_AUTO;
 
 static bool valid_schedule(int s) {
   return s == PNTF_SCHED_AUTO || s == PNTF_SCHED_WAVE_TILE || s == PNTF_SCHED_SPLIT_TILE ||
-         s == PNTF_SCHED_WIDE_TILE;
+         s == PNTF_SCHED_WIDE_TILE || s == PNTF_SCHED_QUAD_TILE;
 }
 
 #ifndef PNTF_BUILD_INFO
@@ -128,9 +151,21 @@ static int check_common(const float* packed, int dim, const float* xp, int64_t n
 }
 
 template <int DIM>
+static void launch_quad(int kind, int64_t grid, const FieldArgs& a, hipStream_t s) {
+  dim3 g((unsigned)grid), b(256);
+  switch (kind) {
+    case K_TAU: hipLaunchKernelGGL((field_quad_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
+    case K_TAU_GRAD: hipLaunchKernelGGL((field_quad_kernel<DIM, K_TAU_GRAD>), g, b, 0, s, a); break;
+    case K_VELOCITY: hipLaunchKernelGGL((field_quad_kernel<DIM, K_VELOCITY>), g, b, 0, s, a); break;
+    case K_SPEED: hipLaunchKernelGGL((field_quad_kernel<DIM, K_SPEED>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((field_quad_kernel<DIM, K_TRAVEL>), g, b, 0, s, a); break;
+  }
+}
+
+template <int DIM>
 static void launch_field(int kind, int64_t grid, const FieldArgs& a, hipStream_t s,
                          bool split, bool wide) {
-  dim3 g((unsigned)grid), b(256);
+  dim3 g((unsigned)grid), b(split ? 64 * SPLIT_WAVES : 256);
   if (wide) {
     switch (kind) {
       case K_TAU: hipLaunchKernelGGL((wide_field_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
@@ -181,6 +216,12 @@ static int run_field(int kind, const float* packed, int dim, const float* xp, in
   if (n == 0) return PNTF_OK;
   if (!out0 || (kind == K_TAU_GRAD && !out1)) return fail(PNTF_ERR_ARG, "null output%s");
   const bool grad = kind != K_TAU && kind != K_TRAVEL;
+  if (use_quad(n, schedule)) {   // σ10 stays in LDS: no workspace
+    FieldArgs a{packed, xp, Btab, env, n, n_env, mode, out0, out1, (float*)ws};
+    if (dim == 3) launch_quad<3>(kind, quad_grid_for(n), a, s);
+    else launch_quad<6>(kind, quad_grid_for(n), a, s);
+    return check_launch("field_quad_kernel");
+  }
   const bool split = use_split(n, schedule);
   const bool wide = !split && schedule != PNTF_SCHED_WAVE_TILE;
   int64_t grid = split ? split_grid_for(n) : wide ? wide_grid_for(n) : grid_for(n);
@@ -224,7 +265,8 @@ int pntf_set_field_schedule(int schedule) {
 size_t pntf_workspace_bytes(int64_t n) {
   if (n <= 0) n = 1;
   int64_t g = grid_for(n), gs = split_grid_for(n);
-  size_t narrow = (size_t)(g > gs ? g : gs) * WAVES * SLOT_BYTES;
+  size_t narrow = (size_t)g * WAVES * SLOT_BYTES, split = (size_t)gs * SPLIT_WAVES * SLOT_BYTES;
+  if (split > narrow) narrow = split;
   size_t wide = (size_t)wide_grid_for(n) * WAVES * WSLOT_BYTES;
   return narrow > wide ? narrow : wide;
 }
@@ -268,6 +310,13 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
     hipLaunchKernelGGL(pack_wide_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx],
                        d.cols, d.rows, d.cols, 1, packed + OFF_WIDE + OFF_BWD + d.off);
   }
+  // the quad streams: every layer of both directions in planner-step order
+  for (int L = 0; L < Q_NL; ++L) {
+    const M& d = mats[Q_LAYERS[L].mat];
+    unsigned blocks = (unsigned)(((int64_t)d.rows * d.cols + 255) / 256);
+    hipLaunchKernelGGL(pack_quad_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx],
+                       d.rows, d.cols, Q_LAYERS[L].dir, packed + OFF_QUAD + q_layer_off(L));
+  }
   struct Bc { int idx, n, off; };
   const Bc bs[] = {
       {1, 128, B_E0},           {3, 128, B_EBLK + 0},     {11, 128, B_EBLK + 128},
@@ -281,6 +330,8 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
   const int aux = W_SZ_BCOL + W_SZ_G4W + 4;
   hipLaunchKernelGGL(pack_wide_aux_kernel, dim3((aux + 255) / 256), dim3(256), 0, stream,
                      packed + OFF_BIAS, packed + OFF_WIDE);
+  hipLaunchKernelGGL(pack_quad_aux_kernel, dim3(Q_WAVES * Q_NAUX), dim3(256), 0, stream,
+                     packed + OFF_BIAS, packed + OFF_QUAD);
   return check_launch("pack_weights");
 }
 
@@ -346,15 +397,22 @@ int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, cons
   if (!valid_schedule(schedule)) return fail(PNTF_ERR_ARG, "unknown schedule%s");
   if (q == 0) return PNTF_OK;
   if (!path || !steps) return fail(PNTF_ERR_ARG, "null output%s");
+  PlanArgs a{packed, xp0, Btab, env, q, n_env, mode, step, tol, max_iter, path, steps,
+             (float*)ws};
+  if (use_quad(q, schedule)) {   // no workspace
+    dim3 g((unsigned)quad_grid_for(q)), b(256);
+    if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((plan_quad_kernel<6>), g, b, 0, stream, a);
+    return check_launch("plan_quad_kernel");
+  }
   if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
   const bool split = use_split(q, schedule);
   int64_t grid;
   st = grid_with_ws(q, ws_bytes, &grid, split);
   if (st) return st;
-  PlanArgs a{packed, xp0, Btab, env, q, n_env, mode, step, tol, max_iter, path, steps,
-             (float*)ws};
   dim3 g((unsigned)grid), b(256);
   if (split) {
+    b = dim3(64 * SPLIT_WAVES);
     if (dim == 3) hipLaunchKernelGGL((plan_split_kernel<3>), g, b, 0, stream, a);
     else hipLaunchKernelGGL((plan_split_kernel<6>), g, b, 0, stream, a);
     return check_launch("plan_split_kernel");

@@ -22,7 +22,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int H = 128;              // hidden width (model_res_sigmoid_multi.py:134)
 constexpr int TILE = 16;            // pairs per wave
-constexpr int WAVES = 4;            // waves per workgroup
+constexpr int WAVES = 4;            // waves per workgroup (one per SIMD)
+// Waves per workgroup of the split-tile kernels (pntf_split.h): one per SIMD.  8 (two per
+// SIMD) builds and is 5 % faster at 16 pairs, but returns wrong ∇τ in pair columns 12-15
+// from the second wave on a SIMD; diagnostics only.
+#ifndef PNTF_SPLIT
+#define PNTF_SPLIT 4
+#endif
+constexpr int SPLIT_WAVES = PNTF_SPLIT;
 // One wave per SIMD: the kernels need up to 512 VGPRs to stay spill-free.  (At two waves per
 // SIMD (256 VGPRs) hipcc spills MFMA results, and on gfx950 those spill stores read the
 // MFMA destination before its last pass lands: corrupt columns 12-15 of 16x16 tiles under
@@ -67,7 +74,46 @@ constexpr int W_OFF_G4W = W_OFF_BCOL + W_SZ_BCOL;
 constexpr int W_SZ_G4W = 16 * 256;
 constexpr int W_OFF_G4B = W_OFF_G4W + W_SZ_G4W;
 constexpr int W_SZ = W_OFF_G4B + 4;
-constexpr int PACKED_TOTAL = OFF_WIDE + W_SZ;
+// Quad blob (pntf_quad.h, v_mfma_f32_4x4x1_16b_f32 on 4-pair tiles), packed after the wide
+// one: per wave of a workgroup, the fragments of its quarter of every layer's out rows in
+// the order a planner step consumes them (13 forward layers, then the 13 reverse ones), so
+// the weight ring is one linear stream; then per wave 14 bias vectors (the 13 forward
+// layers' biases and the head row, in the wave's compact row order).
+constexpr int Q_WAVES = 4;
+constexpr int Q_NL = 26;
+constexpr int Q_STREAM = 2 * SZ_DIR / Q_WAVES;      // floats of one wave's fragment stream
+constexpr int Q_NF_FWD = SZ_DIR / Q_WAVES / 256;    // 1 KiB fragments of its forward part
+constexpr int Q_NAUX = 14;
+constexpr int OFF_QUAD = (OFF_WIDE + W_SZ + 63) / 64 * 64;
+constexpr int Q_OFF_AUX = Q_WAVES * Q_STREAM;
+constexpr int Q_SZ = Q_OFF_AUX + Q_WAVES * Q_NAUX * 256;
+constexpr int PACKED_TOTAL = OFF_QUAD + Q_SZ;
+// Quad layer list in stream order: packed matrix (0..12, the OFF_* order above), direction
+// (0: A = W, 1: A = W^T), out rows, in features, plain bias offset (forward layers).
+struct QLayer {
+  int mat, dir, out, in, bias;
+};
+constexpr QLayer Q_LAYERS[Q_NL] = {
+    {0, 0, 128, 256, B_E0},          {1, 0, 128, 128, B_EBLK},
+    {2, 0, 128, 128, B_EBLK + 128},  {3, 0, 128, 128, B_EBLK + 256},
+    {4, 0, 128, 128, B_EBLK + 384},  {5, 0, 128, 128, B_E3},
+    {6, 0, 256, 256, B_GBLK},        {7, 0, 256, 256, B_GBLK + 256},
+    {8, 0, 256, 256, B_GBLK + 512},  {9, 0, 256, 256, B_GBLK + 768},
+    {10, 0, 256, 256, B_GBLK + 1024}, {11, 0, 256, 256, B_GBLK + 1280},
+    {12, 0, 128, 256, B_G3},
+    {12, 1, 256, 128, -1}, {11, 1, 256, 256, -1}, {10, 1, 256, 256, -1},
+    {9, 1, 256, 256, -1},  {8, 1, 256, 256, -1},  {7, 1, 256, 256, -1},
+    {6, 1, 256, 256, -1},  {5, 1, 128, 128, -1},  {4, 1, 128, 128, -1},
+    {3, 1, 128, 128, -1},  {2, 1, 128, 128, -1},  {1, 1, 128, 128, -1},
+    {0, 1, 256, 128, -1}};
+// Start of layer L in a wave's stream (floats).
+constexpr int q_layer_off(int L) {
+  int o = 0;
+  for (int i = 0; i < L; ++i) o += Q_LAYERS[i].out * Q_LAYERS[i].in / Q_WAVES;
+  return o;
+}
+static_assert(q_layer_off(Q_NL) == Q_STREAM, "quad stream covers both directions");
+static_assert(q_layer_off(13) == Q_NF_FWD * 256, "forward part of the quad stream");
 
 // ---------------------------------------------------------------- per-wave scratch (saved σ10)
 // Each saved "tile" is 16 feature rows x 16 pairs = 256 floats, stored lane-major

@@ -276,6 +276,9 @@ __device__ __forceinline__ void store_tile(Scratch sc, int tile, int lane, f32x4
   asm volatile("" ::"v"(v));
   return;
 #endif
+#ifdef PNTF_DIAG_STORENOP  // diagnostics only (tests/diag split variants)
+  asm volatile("s_nop 7\n\ts_nop 7" ::"v"(v));
+#endif
   __builtin_amdgcn_raw_buffer_store_b128(
       __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), sc.r, lane * 16,
       tile * 1024, AUX_NT);
@@ -411,6 +414,9 @@ struct Tail {
 // ... or run at once.
 template <class L>
 __device__ __forceinline__ void flush(L& ly) {
+#ifdef PNTF_DIAG_EPINOP   // diagnostics only (tests/diag split variants)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#endif
   Tail<L> t{ly};
   static_for<0, L::NO * L::NC * L::EPS>([&](auto j) { t(j); });
 }

@@ -5,13 +5,20 @@
 //   -DPNTF_PLAN -DPNTF_DIM=3|6         plan_kernel<DIM>
 //   -DPNTF_PLAN_SPLIT -DPNTF_DIM=3|6   plan_split_kernel<DIM> (pntf_split.h)
 //   -DPNTF_RESIDUAL -DPNTF_DIM=3|6     residual_kernel<DIM> (Taylor mode, pntf_taylor.h)
-//   -DPNTF_UTIL                        pack_kernel, copy_kernel, sum_kernel, wide packing
+//   -DPNTF_KIND=0..4 -DPNTF_DIM=3|6 -DPNTF_QUAD_FIELD    field_quad_kernel<DIM, KIND> (pntf_quad.h)
+//   -DPNTF_PLAN_QUAD -DPNTF_DIM=3|6    plan_quad_kernel<DIM> (pntf_quad.h)
+//   -DPNTF_UTIL                        pack_kernel, copy_kernel, sum_kernel, wide / quad packing
+#include "pntf_quad.h"
 #include "pntf_split.h"
 #include "pntf_taylor.h"
 #include "pntf_wide.h"
 
 namespace pntf {
-#if defined(PNTF_KIND) && defined(PNTF_WIDE_FIELD)
+#if defined(PNTF_KIND) && defined(PNTF_QUAD_FIELD)
+template __global__ void field_quad_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
+#elif defined(PNTF_PLAN_QUAD)
+template __global__ void plan_quad_kernel<PNTF_DIM>(PlanArgs);
+#elif defined(PNTF_KIND) && defined(PNTF_WIDE_FIELD)
 template __global__ void wide_field_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
 #elif defined(PNTF_KIND) && defined(PNTF_SPLIT_FIELD)
 template __global__ void field_split_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);

@@ -1,0 +1,563 @@
+#pragma once
+// Quad-tile τ / ∇τ / planner kernels for batches of a few queries.
+//
+// A planner step streams both weight directions (4.33 MB) through the CU that owns the query
+// tile, so its time is bounded below by one CU's weight-stream rate (tests/diag/stream_probe:
+// ≈42 µs per step at ≈103 GB/s per CU) and by the tile's MFMA work.  On 16-pair tiles the
+// MFMA work alone is ≈68 µs per step on one CU (16x16x4: 16 pairs per instruction), and a
+// 1024-query plan (BASELINE C5) keeps only 64 CUs busy.  Here a tile is 4 pairs and the
+// matrix op is v_mfma_f32_4x4x1_16b_f32 (16 independent 4x4x1 blocks per instruction):
+//   * blocks b = 4·og + kb: og picks 4 of the instruction's 16 out rows, kb one of its 4 k;
+//     A lane l = W[r0 + 4·og + (l & 3)][k0 + kb], B lane l = act[k0 + kb][pair l & 3], so
+//     one instruction is 16 out rows x 4 k x 4 pairs and the accumulators hold one partial
+//     sum per k sub-block (kb), summed over the row (two DPP row_ror adds) after the layer;
+//   * the four waves of the workgroup (one per SIMD) own a quarter of every layer's out
+//     rows; after the sum each lane keeps one (row, pair) value ("compact": row
+//     r0 + 4·og + kb, pair l & 3), runs the epilogue on it and writes it to an LDS
+//     activation buffer laid out for the next layer's B reads (one ds_read_b128 per 4 k and
+//     column, conflict-free), then one workgroup barrier per layer;
+//   * the saved σ10 values stay in LDS (compact, per wave), so there is no global scratch;
+//   * each wave's weight fragments are packed in consumption order (pntf_common.h Q_LAYERS),
+//     so the prefetch ring is one linear stream of 1 KiB fragments, 8 in flight, that wraps
+//     from the last reverse layer into the next step's encoder[0].
+// 1024 queries are 256 tiles: every CU of the chip has one.  Reductions whose result every
+// lane consumes (τ, ∇τ) use xor butterflies and a fixed wave order, so all lanes of a pair
+// hold bitwise identical values and the planner's freeze/exit decisions agree in all waves.
+#include "pntf_split.h"
+
+namespace pntf {
+
+constexpr int QPAIRS = 4;
+// independent accumulator chains per column (k steps alternate between them)
+#ifndef PNTF_Q_CHAINS
+#define PNTF_Q_CHAINS 2
+#endif
+constexpr int QCH = PNTF_Q_CHAINS;
+#ifndef PNTF_QRING
+#define PNTF_QRING 16
+#endif
+constexpr int QRING = PNTF_QRING;           // fragments in flight per wave
+constexpr int Q_NF_ALL = 2 * Q_NF_FWD;
+constexpr int QBUF = 2 * 16 * 68;           // activation buffer: 2 columns x 16 lane rows x 68
+constexpr int QNSIG = 48;                   // saved σ10 slots per wave (64 floats each)
+constexpr int Q_RED = 3 * QBUF + Q_WAVES * QNSIG * 64;
+// 21504 floats = 84 KiB: more than half the CU's LDS, so one workgroup per CU (the second
+// wave per SIMD corrupts MFMA results here)
+constexpr int Q_LDS_FLOATS = 21504;
+static_assert(Q_RED + Q_WAVES * 12 * 4 <= Q_LDS_FLOATS, "quad LDS budget");
+// σ slots (forward order): encoder[0] 0-3, encoder blocks a0 4-7, b0 8-11, a1 12-15,
+// b1 16-19 (group·2 + column), merge switch 20-21, generator a_i 22 + 8i + g, b_i 26 + 8i + g,
+// generator[-2] 46-47.
+constexpr int QS_E0 = 0, QS_EBLK = 4, QS_S0 = 20, QS_GBLK = 22, QS_G3 = 46;
+
+__device__ __forceinline__ void qsync() {
+#ifndef PNTF_QABL_NOBAR   // diagnostics only (tests/diag timing ablations; wrong results)
+  wg_sync();
+#endif
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+// v + v(lane rotated by N within its 16-lane row)
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                           0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+// x ^ mask lane exchange inside 32-lane halves (ds_swizzle bit mode)
+template <int MASK>
+__device__ __forceinline__ float swz_xor(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v),
+                                                                0x1f | (MASK << 10)));
+}
+// Sum over the 16 lanes of the same pair (lane bits 2-5), identical in all of them: xor
+// butterflies (a + b == b + a bitwise).
+__device__ __forceinline__ float pair_sum(float v) {
+  v += swz_xor<4>(v);
+  v += swz_xor<8>(v);
+  v += swz_xor<16>(v);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+// v[g] for a runtime group index (explicit selects: a dynamic vector index would put the
+// vector on the stack)
+__device__ __forceinline__ float pick(const f32x4& v, int g) {
+  return g == 0 ? v[0] : g == 1 ? v[1] : g == 2 ? v[2] : v[3];
+}
+
+struct QCx {
+  lds_f* lds;
+  int w, lane, og, kb, l16;
+  __device__ lds_f* buf(int b) const { return lds + b * QBUF; }
+  __device__ lds_f* sig(int slot) const { return lds + 3 * QBUF + (w * QNSIG + slot) * 64 + lane; }
+  __device__ lds_f* red(int wave, int v) const { return lds + Q_RED + (wave * 12 + v) * 4; }
+  // compact (row, pair) slot of a layer with OUT rows, group g, column c in a buffer read by
+  // the next layer (its in features = OUT: row stride OUT/4 + 4)
+  template <int OUT>
+  __device__ lds_f* at(lds_f* b, int c, int g) const {
+    return b + (c * 16 + l16) * (OUT / 4 + 4) + w * (OUT / 16) + 4 * g + og;
+  }
+};
+
+struct QRing {
+  f32x4 r[QRING];
+  int next;   // next fragment to load (wave-uniform)
+};
+template <int NF>
+__device__ __forceinline__ void qfetch(QRing& ring, Rsrc W, int lane, int slot) {
+#ifdef PNTF_QABL_NOLOAD   // diagnostics only (tests/diag timing ablations; wrong results)
+  ring.r[slot] = ring.r[slot] * 1.0001f;
+#else
+  ring.r[slot] = bload(W, lane * 16, ring.next * 1024);
+#endif
+  ring.next = ring.next + 1 == NF ? 0 : ring.next + 1;
+}
+
+// One layer: `groups` groups of 16 out rows; per group IN/16 fragments of 4 k steps x NC
+// columns; B operands read from `in` (IN features, row stride IN/4 + 4).  epi(g, v[NC]) gets
+// the compact sums of group g.
+template <int NC, int IN, int NF, class Epi>
+__device__ __forceinline__ void qlayer(QRing& ring, Rsrc W, const QCx& cx, const lds_f* in,
+                                       int groups, Epi&& epi) {
+  constexpr int SP = IN / 4 + 4, NQ = IN / 16;
+  // U groups per loop trip, so every trip starts at ring slot 0
+  constexpr int U = NQ >= QRING ? 1 : QRING / NQ;
+  static_assert((U * NQ) % QRING == 0, "a loop trip starts at ring slot 0");
+  const lds_f* src = in + cx.l16 * SP;
+#pragma unroll 1
+  for (int g0 = 0; g0 < groups; g0 += U) static_for<0, U>([&](auto uu) {
+    constexpr int u = decltype(uu)::value;
+    const int g = g0 + u;
+    f32x4 acc[NC][QCH];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int h = 0; h < QCH; ++h) acc[c][h] = zero4();
+    static_for<0, NQ>([&](auto qq) {
+      constexpr int q = decltype(qq)::value, slot = (u * NQ + q) % QRING;
+      f32x4 b[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+#ifdef PNTF_QABL_NOLDS   // diagnostics only (tests/diag timing ablations; wrong results)
+        b[c] = f32x4{0.1f * q, 0.2f * c, 0.3f, 0.4f} + (float)cx.lane;
+#else
+        b[c] = *reinterpret_cast<const lds_f4*>(src + c * 16 * SP + 4 * q);
+#endif
+      }
+      const f32x4 a = ring.r[slot];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c][e % QCH] = mfma4(a[e], b[c][e], acc[c][e % QCH]);
+      qfetch<NF>(ring, W, cx.lane, slot);
+    });
+    float v[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      f32x4 s;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t = acc[c][0][i];
+#pragma unroll
+        for (int h = 1; h < QCH; ++h) t += acc[c][h][i];
+        s[i] = dpp_add<0x128>(dpp_add<0x124>(t));
+      }
+      v[c] = cx.kb == 0 ? s[0] : cx.kb == 1 ? s[1] : cx.kb == 2 ? s[2] : s[3];
+    }
+    epi(g, v);
+  });
+}
+
+// Sum of NV per-lane values over the pair's 16 lanes and the 4 waves (fixed order); the
+// result is identical in every lane of the pair in every wave.
+template <int NV>
+__device__ __forceinline__ void qreduce(const QCx& cx, float (&v)[NV]) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = pair_sum(v[i]);
+  if (cx.lane < QPAIRS)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) cx.red(cx.w, i)[cx.lane] = v[i];
+  qsync();
+  const int j = cx.lane & 3;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float s = cx.red(0, i)[j];
+#pragma unroll
+    for (int q = 1; q < Q_WAVES; ++q) s += cx.red(q, i)[j];
+    v[i] = s;
+  }
+}
+
+// Forward pass (NN.out, :215-259) for the 4 pairs of the tile; returns τ of the lane's pair.
+// GRAD: save σ10 for the reverse sweep.  Buffers: 0 = features / dz, 1 = A, 2 = B.
+template <int DIM, bool GRAD, int NF>
+__device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx,
+                                              const PairIO& io, const f32x4 (&aux)[Q_NAUX],
+                                              int compat) {
+  const float cm = compat ? 1.f : 0.f;
+  lds_f *F = cx.buf(0), *A = cx.buf(1), *B = cx.buf(2);
+  const int t = cx.w * 64 + cx.lane;
+  // ---- Fourier features (:186-190): thread t computes column (t >> 2) & 1 of its lane's
+  // pair for features t >> 3 + 32 m; sin f -> k = f, cos f -> k = f + 128
+  {
+    const int c = (t >> 2) & 1, j = t & 3, fb = t >> 3;
+    float xc[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) xc[d] = c ? io.x[1][d] : io.x[0][d];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int f = fb + 32 * m;
+      float q = 0.f;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) q = fmaf(xc[d], TWO_PI * io.Bw[d * H + f], q);
+      float sn, cs;
+      sincos_fast(q, sn, cs);
+      lds_f* p = F + (c * 16 + 4 * (f & 3) + j) * 68 + (f >> 2);
+      p[0] = sn;
+      p[32] = cs;
+    }
+  }
+  qsync();
+  // ---- encoder[0] (:227); compat: the out_backgrad quirk (:435-438) stores σ10(softplus(y))
+  qlayer<2, 256, NF>(ring, W, cx, F, 2, [&](int g, const float (&v)[2]) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      SpSig q = sp_sig(v[c] + pick(aux[0], g));
+      *cx.at<128>(A, c, g) = q.sp;
+      if (GRAD) *cx.sig(QS_E0 + 2 * g + c) = fmaf(cm, __builtin_amdgcn_rcpf(2.f - q.sg) - q.sg, q.sg);
+    }
+  });
+  qsync();
+  // ---- encoder residual blocks (:228-232): a: A -> B, b: B (+ A residual) -> A
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int la = 1 + 2 * blk, sa = QS_EBLK + 8 * blk;
+    qlayer<2, 128, NF>(ring, W, cx, A, 2, [&](int g, const float (&v)[2]) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        SpSig q = sp_sig(v[c] + pick(aux[la], g));
+        *cx.at<128>(B, c, g) = q.sp;
+        if (GRAD) *cx.sig(sa + 2 * g + c) = q.sg;
+      }
+    });
+    qsync();
+    qlayer<2, 128, NF>(ring, W, cx, B, 2, [&](int g, const float (&v)[2]) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        lds_f* o = cx.at<128>(A, c, g);
+        SpSig q = sp_sig(v[c] + pick(aux[la + 1], g) + *o);
+        *o = q.sp;
+        if (GRAD) *cx.sig(sa + 4 + 2 * g + c) = q.sg;
+      }
+    });
+    qsync();
+  }
+  // ---- encoder[-1] (:234) and the smooth max / min merge (:236-244): u = [M | m] -> B
+  qlayer<2, 128, NF>(ring, W, cx, A, 2, [&](int g, const float (&v)[2]) {
+    const float zs = v[0] + pick(aux[5], g), zg = v[1] + pick(aux[5], g);
+    const float d = zs - zg;
+    const float e = exp_neg10abs(d);
+    const float cc = 0.1f * log1p_small(e);
+    lds_f* o = cx.at<256>(B, 0, g) - cx.w * 8;   // row r of a 128-row layer in a 256-row buffer
+    o[0] = fmaxf(zs, zg) + cc;
+    o[32] = fminf(zs, zg) - cc;
+    if (GRAD) {
+      const float rr = __builtin_amdgcn_rcpf(1.f + e);
+      *cx.sig(QS_S0 + g) = (d >= 0.f) ? rr : e * rr;
+    }
+  });
+  qsync();
+  // ---- generator residual blocks (:246-249): a: B -> A, b: A (+ B residual) -> B
+#pragma unroll 1
+  for (int i = 0; i < 3; ++i) {
+    const f32x4 ba = i == 0 ? aux[6] : i == 1 ? aux[8] : aux[10];
+    const f32x4 bb = i == 0 ? aux[7] : i == 1 ? aux[9] : aux[11];
+    qlayer<1, 256, NF>(ring, W, cx, B, 4, [&](int g, const float (&v)[1]) {
+      SpSig q = sp_sig(v[0] + pick(ba, g));
+      *cx.at<256>(A, 0, g) = q.sp;
+      if (GRAD) *cx.sig(QS_GBLK + 8 * i + g) = q.sg;
+    });
+    qsync();
+    qlayer<1, 256, NF>(ring, W, cx, A, 4, [&](int g, const float (&v)[1]) {
+      lds_f* o = cx.at<256>(B, 0, g);
+      SpSig q = sp_sig(v[0] + pick(bb, g) + *o);
+      *o = q.sp;
+      if (GRAD) *cx.sig(QS_GBLK + 8 * i + 4 + g) = q.sg;
+    });
+    qsync();
+  }
+  // ---- generator[-2] + act (:251-252) and the head generator[-1] (:254-255)
+  float part[1] = {0.f};
+  qlayer<1, 256, NF>(ring, W, cx, B, 2, [&](int g, const float (&v)[1]) {
+    SpSig q = sp_sig(v[0] + pick(aux[12], g));
+    part[0] = fmaf(pick(aux[13], g), q.sp, part[0]);
+    if (GRAD) *cx.sig(QS_G3 + g) = q.sg;
+  });
+  qreduce<1>(cx, part);
+  const float y4 = part[0] + aux[13][2];
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-0.144269504088896341f * y4));
+}
+
+// Reverse sweep (exact, or out_backgrad when the forward stored the quirk): dτ/dxs, dτ/dxg of
+// the lane's pair, identical in all lanes of the pair.
+template <int DIM, int NF>
+__device__ __forceinline__ void quad_backward(QRing& ring, Rsrc W, const QCx& cx,
+                                              const PairIO& io, float tau,
+                                              const f32x4 (&aux)[Q_NAUX], float (&ds)[DIM],
+                                              float (&dg)[DIM]) {
+  lds_f *F = cx.buf(0), *A = cx.buf(1), *B = cx.buf(2);
+  // ---- head and generator[-2] (:592-613): dv = d · G4 ⊙ σ10(y3) -> A (128 rows)
+  const float dd = 0.1f * tau * (1.f - tau);
+#pragma unroll
+  for (int g = 0; g < 2; ++g) *cx.at<128>(A, 0, g) = dd * pick(aux[13], g) * *cx.sig(QS_G3 + g);
+  qsync();
+  // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> B
+  qlayer<1, 128, NF>(ring, W, cx, A, 4, [&](int g, const float (&v)[1]) {
+    *cx.at<256>(B, 0, g) = v[0] * *cx.sig(QS_GBLK + 16 + 4 + g);
+  });
+  qsync();
+  // ---- generator blocks, reverse (:615-618): lb: B -> A, la: A (+ B residual) -> B
+#pragma unroll 1
+  for (int i = 2; i >= 0; --i) {
+    qlayer<1, 256, NF>(ring, W, cx, B, 4, [&](int g, const float (&v)[1]) {
+      *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * i + g);
+    });
+    qsync();
+    const int sb = QS_GBLK + 8 * (i - 1) + 4;   // σ10(y2) of block i - 1 (none for i = 0)
+    qlayer<1, 256, NF>(ring, W, cx, A, 4, [&](int g, const float (&v)[1]) {
+      lds_f* o = cx.at<256>(B, 0, g);
+      const float y = v[0] + *o;
+      *o = i > 0 ? y * *cx.sig(sb + g) : y;
+    });
+    qsync();
+  }
+  // ---- merge Jacobian (:620-627) on the wave's 128-row share: dz -> F (2 columns)
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const lds_f* u = cx.at<256>(B, 0, g) - cx.w * 8;   // row r of the 128-row map
+    const float dM = u[0], dm = u[32];
+    const float s0 = *cx.sig(QS_S0 + g), s1 = 1.f - s0;
+    *cx.at<128>(F, 0, g) = s0 * dM + s1 * dm;
+    *cx.at<128>(F, 1, g) = s1 * dM + s0 * dm;
+  }
+  qsync();
+  // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1): F -> A
+  qlayer<2, 128, NF>(ring, W, cx, F, 2, [&](int g, const float (&v)[2]) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) *cx.at<128>(A, c, g) = v[c] * *cx.sig(QS_EBLK + 12 + 2 * g + c);
+  });
+  qsync();
+  // ---- encoder blocks, reverse (:633-636): b^T: A -> B (⊙ σ10(y1)), a^T: B (+ A) -> A
+  // (⊙ σ10 of the layer below: block 0's y2, or encoder[0])
+#pragma unroll
+  for (int blk = 1; blk >= 0; --blk) {
+    const int sa = QS_EBLK + 8 * blk, sbelow = blk ? QS_EBLK + 4 : QS_E0;
+    qlayer<2, 128, NF>(ring, W, cx, A, 2, [&](int g, const float (&v)[2]) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) *cx.at<128>(B, c, g) = v[c] * *cx.sig(sa + 2 * g + c);
+    });
+    qsync();
+    qlayer<2, 128, NF>(ring, W, cx, B, 2, [&](int g, const float (&v)[2]) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        lds_f* o = cx.at<128>(A, c, g);
+        *o = (v[c] + *o) * *cx.sig(sbelow + 2 * g + c);
+      }
+    });
+    qsync();
+  }
+  // ---- encoder[0]^T fused with the Fourier Jacobian (:639-645): the wave's 64 feature rows
+  // f (sin rows f < 128 in waves 0-1, cos rows in waves 2-3), both columns
+  float acc[2 * DIM];
+#pragma unroll
+  for (int i = 0; i < 2 * DIM; ++i) acc[i] = 0.f;
+  qlayer<2, 128, NF>(ring, W, cx, A, 4, [&](int g, const float (&v)[2]) {
+    const int f = cx.w * 64 + 16 * g + 4 * cx.og + cx.kb;
+    const int fb = f & 127;
+    float bw[DIM];
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) bw[d] = TWO_PI * io.Bw[d * H + fb];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      float q = 0.f;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], bw[d], q);
+      float sn, cs;
+      sincos_fast(q, sn, cs);
+      const float gg = f < 128 ? v[c] * cs : -(v[c] * sn);
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) acc[c * DIM + d] = fmaf(bw[d], gg, acc[c * DIM + d]);
+    }
+  });
+  qreduce<2 * DIM>(cx, acc);
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) {
+    ds[d] = acc[d];
+    dg[d] = acc[DIM + d];
+  }
+}
+
+__device__ __forceinline__ QCx quad_cx(lds_f* lds) {
+  QCx cx;
+  cx.lds = lds;
+  cx.lane = threadIdx.x & 63;
+  cx.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  cx.og = cx.lane >> 4;
+  cx.kb = (cx.lane >> 2) & 3;
+  cx.l16 = cx.lane & 15;
+  return cx;
+}
+
+// τ / ∇τ / epilogues on quad tiles: one workgroup per 4-pair tile (grid-stride), same
+// outputs as field_kernel<DIM, KIND>.
+template <int DIM, int KIND>
+__global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
+  constexpr bool GRAD = KIND != K_TAU && KIND != K_TRAVEL;
+  constexpr int NF = GRAD ? Q_NF_ALL : Q_NF_FWD;
+  __shared__ float smem[Q_LDS_FLOATS];
+  const QCx cx = quad_cx((lds_f*)smem);
+  const Rsrc W = make_rsrc(a.P + OFF_QUAD + cx.w * Q_STREAM, Q_STREAM * 4);
+  const Rsrc AX = make_rsrc(a.P + OFF_QUAD + Q_OFF_AUX + cx.w * Q_NAUX * 256, Q_NAUX * 1024);
+  f32x4 aux[Q_NAUX];
+#pragma unroll
+  for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
+  aux[13][2] = a.P[OFF_BIAS + B_G4B];
+  QRing ring;
+  ring.next = 0;
+#pragma unroll
+  for (int s = 0; s < QRING; ++s) qfetch<NF>(ring, W, cx.lane, s);
+  const int64_t ntiles = (a.n + QPAIRS - 1) / QPAIRS;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t pair = tile * QPAIRS + (cx.lane & 3);
+    PairIO io;
+    const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
+    const float tau = quad_forward<DIM, GRAD, NF>(ring, W, cx, io, aux, a.compat);
+    float ds[DIM], dg[DIM];
+    if constexpr (GRAD) quad_backward<DIM, NF>(ring, W, cx, io, tau, aux, ds, dg);
+    const bool store = cx.w == 0 && cx.lane < QPAIRS && pair < a.n;
+    store_field<DIM, KIND>(a, pair, ok, store, tau, io, ds, dg);
+  }
+}
+
+// Batched planner on quad tiles: one workgroup per 4-query tile (grid-stride), the loop of
+// plan_kernel (test/gib_plan.py:74-86, test/arm_plan.py:140-152) with per-query freeze.
+template <int DIM>
+__global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
+  __shared__ float smem[Q_LDS_FLOATS];
+  const QCx cx = quad_cx((lds_f*)smem);
+  const Rsrc W = make_rsrc(a.P + OFF_QUAD + cx.w * Q_STREAM, Q_STREAM * 4);
+  const Rsrc AX = make_rsrc(a.P + OFF_QUAD + Q_OFF_AUX + cx.w * Q_NAUX * 256, Q_NAUX * 1024);
+  f32x4 aux[Q_NAUX];
+#pragma unroll
+  for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
+  aux[13][2] = a.P[OFF_BIAS + B_G4B];
+  QRing ring;
+  ring.next = 0;
+#pragma unroll
+  for (int s = 0; s < QRING; ++s) qfetch<Q_NF_ALL>(ring, W, cx.lane, s);
+  const int cap = a.max_iter + 1;
+  const int64_t rows = (int64_t)cap + 1;
+  const int64_t ntiles = (a.q + QPAIRS - 1) / QPAIRS;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t qi = tile * QPAIRS + (cx.lane & 3);
+    PairIO io;
+    const bool ok = load_pair<DIM>(a.xp0, a.Btab, a.env, a.q, a.n_env, qi, io);
+    const bool store = cx.w == 0 && cx.lane < QPAIRS && qi < a.q;
+    float* prow = a.path + (store ? qi : 0) * rows * 2 * DIM;
+    auto dist = [&]() {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) {
+        float D = io.x[1][d] - io.x[0][d];
+        s = fmaf(D, D, s);
+      }
+      return sqrtf(s);
+    };
+    bool active = ok && dist() > a.tol;
+    if (store) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) prow[c * DIM + d] = io.x[c][d];
+    }
+    int nsteps = 0;
+    int it = 0;
+    for (; it < cap; ++it) {
+      if (!__any(active)) break;
+      const float tau = quad_forward<DIM, true, Q_NF_ALL>(ring, W, cx, io, aux, a.compat);
+      float ds[DIM], dg[DIM], vs[DIM], vg[DIM];
+      quad_backward<DIM, Q_NF_ALL>(ring, W, cx, io, tau, aux, ds, dg);
+      path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
+      if (active) {
+#pragma unroll
+        for (int d = 0; d < DIM; ++d) {
+          io.x[0][d] = io.x[0][d] + a.step * vs[d];
+          io.x[1][d] = io.x[1][d] + a.step * vg[d];
+        }
+        ++nsteps;
+        if (!(dist() > a.tol)) active = false;
+      }
+      if (store) {
+        float* pr = prow + (int64_t)(it + 1) * 2 * DIM;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) pr[c * DIM + d] = io.x[c][d];
+      }
+    }
+    if (store) {
+      for (int64_t r = it + 1; r < rows; ++r) {
+        float* pr = prow + r * 2 * DIM;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) pr[c * DIM + d] = io.x[c][d];
+      }
+      a.steps[qi] = ok ? nsteps : -1;
+    }
+  }
+}
+
+#if defined(PNTF_UTIL)
+// ---------------------------------------------------------------- quad weight packing
+// Layer L of wave w: dst[w·Q_STREAM + r], r = ((g·IN/16 + q)·64 + l)·4 + e holds
+// A[w·OUT/4 + 16 g + 4 (l >> 4) + (l & 3)][16 q + 4 e + ((l >> 2) & 3)], A = M (dir 0) or
+// M^T (dir 1) of the rows x cols matrix M.
+__global__ void pack_quad_kernel(const float* __restrict__ src, int rows, int cols, int dir,
+                                 float* __restrict__ dst) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= (int64_t)rows * cols) return;
+  const int OUT = dir ? cols : rows, IN = dir ? rows : cols;
+  const int per = OUT / Q_WAVES * IN;
+  const int w = (int)(o / per), r = (int)(o % per);
+  const int e = r & 3, l = (r >> 2) & 63, fq = r >> 8;
+  const int g = fq / (IN / 16), q = fq % (IN / 16);
+  const int row = w * (OUT / Q_WAVES) + 16 * g + 4 * (l >> 4) + (l & 3);
+  const int k = 16 * q + 4 * e + ((l >> 2) & 3);
+  dst[(int64_t)w * Q_STREAM + r] = dir ? src[(int64_t)k * cols + row] : src[(int64_t)row * cols + k];
+}
+// Bias vectors: aux[w][L][l][g] = bias_L[w·OUT/4 + 16 g + 4 (l >> 4) + ((l >> 2) & 3)] for the
+// 13 forward layers, and the head row generator.4.weight (L = 13) for the 128 rows of
+// generator[-2]; unused groups are 0.
+__global__ void pack_quad_aux_kernel(const float* __restrict__ plain, float* __restrict__ quad) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= Q_WAVES * Q_NAUX * 256) return;
+  const int g = o & 3, l = (o >> 2) & 63, L = (o >> 8) % Q_NAUX, w = o / (Q_NAUX * 256);
+  constexpr int outs[Q_NAUX] = {128, 128, 128, 128, 128, 128, 256, 256, 256, 256, 256, 256, 128,
+                                128};
+  constexpr int offs[Q_NAUX] = {Q_LAYERS[0].bias,  Q_LAYERS[1].bias,  Q_LAYERS[2].bias,
+                                Q_LAYERS[3].bias,  Q_LAYERS[4].bias,  Q_LAYERS[5].bias,
+                                Q_LAYERS[6].bias,  Q_LAYERS[7].bias,  Q_LAYERS[8].bias,
+                                Q_LAYERS[9].bias,  Q_LAYERS[10].bias, Q_LAYERS[11].bias,
+                                Q_LAYERS[12].bias, B_G4W};
+  const int out = outs[L], off = offs[L];
+  float v = 0.f;
+  if (g < out / 64)
+    v = plain[off + w * (out / Q_WAVES) + 16 * g + 4 * (l >> 4) + ((l >> 2) & 3)];
+  quad[Q_OFF_AUX + o] = v;
+}
+#endif  // PNTF_UTIL
+
+}  // namespace pntf

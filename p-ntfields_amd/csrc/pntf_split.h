@@ -24,10 +24,38 @@
 
 namespace pntf {
 
-constexpr int SPLIT = WAVES;                  // waves sharing a pair tile
+// Waves sharing a pair tile: 4 (one per SIMD).  The code is written for 8 as well (two per
+// SIMD, so one wave's exchange and epilogue could run beside the other's MFMAs); that build is
+// kept for diagnostics only (pntf_common.h PNTF_SPLIT).
+constexpr int SPLIT = SPLIT_WAVES;
+static_assert(SPLIT == 4 || SPLIT == 8, "split width");
+constexpr int EOTL = 8 / SPLIT;    // local out tiles of an encoder layer (OT 8, 2 columns)
+constexpr int GOTL = 16 / SPLIT;   // ... of a generator layer (OT 16)
+constexpr int G3OTL = 8 / SPLIT;   // ... of generator[-2] (OT 8)
+constexpr int FKL = 8 / SPLIT;     // Fourier feature tiles of the fold per wave (8 in all)
+constexpr int GNL = GOTL < 4 ? GOTL : 4;   // weight fragments per step of a generator layer
 constexpr int XBUF_FLOATS = 16 * 256;         // one activation: 16 tiles x 64 lanes x 4
 constexpr int RED_FLOATS = SPLIT * 12 * 64;   // cross-wave partial sums (≤ 2·DIM per lane)
 constexpr int SPLIT_LDS_FLOATS = 2 * XBUF_FLOATS + RED_FLOATS;
+
+#ifdef PNTF_DEBUG_DUMP   // diagnostics only (tests/diag/split_dump.py)
+__device__ float* pntf_dbg;
+#ifndef PNTF_DUMP_WAVE
+#define PNTF_DUMP_WAVE 0
+#endif
+#define PNTF_DUMPT(k, i, v)                                                            \
+  if (blockIdx.x == 0 && sp.w == PNTF_DUMP_WAVE && pntf_dbg)                           \
+    *reinterpret_cast<f32x4*>(pntf_dbg + (((k) * 16 + (i)) * 64 + sp.lane) * 4) = (v);
+#define PNTF_DUMPW(k, i, v)                                                            \
+  if (blockIdx.x == 0 && pntf_dbg)                                                     \
+    *reinterpret_cast<f32x4*>(pntf_dbg + ((((k) + sp.w) * 16 + (i)) * 64 + sp.lane) * 4) = (v);
+#define PNTF_DUMPX(k) \
+  for (int i_ = 0; i_ < 16; ++i_) { PNTF_DUMPT(k, i_, X[i_]) }
+#else
+#define PNTF_DUMPT(k, i, v)
+#define PNTF_DUMPW(k, i, v)
+#define PNTF_DUMPX(k)
+#endif
 
 typedef __attribute__((address_space(3))) float lds_f;
 typedef __attribute__((address_space(3))) f32x4 lds_f4;
@@ -58,10 +86,18 @@ __device__ __forceinline__ void exchange(const Split& sp, int buf, const f32x4 (
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
-    for (int t = 0; t < OTL; ++t) *sp.tile(buf, c * OTG + sp.w * OTL + t) = L[c * OTL + t];
+    for (int t = 0; t < OTL; ++t) {
+#ifdef PNTF_DIAG_EXNOP   // diagnostics only (tests/diag split variants)
+      asm volatile("s_nop 7\n\ts_nop 7" ::"v"(L[c * OTL + t]));
+#endif
+      *sp.tile(buf, c * OTG + sp.w * OTL + t) = L[c * OTL + t];
+    }
   wg_sync();
 #pragma unroll
   for (int i = 0; i < NC * OTG; ++i) X[i] = *sp.tile(buf, i);
+#ifdef PNTF_DIAG_EXNOP
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 7" ::: "memory");
+#endif
 }
 
 // The wave's slice of a full bank: R[c·OTL + t] = X[c·OTG + w·OTL + t] (w is uniform).
@@ -106,12 +142,12 @@ __device__ __forceinline__ int wofs(int w) {
   return w * (OTG / SPLIT) * KT * 1024;
 }
 
-// Ring head of the split forward pass: encoder[0], local out tiles 2w, 2w + 1; step j reads
-// fragments (local out tile j % 2, k tile j / 2 + 8 l).
+// Ring head of the split forward pass: encoder[0], local out tiles EOTL·w + o; step j reads
+// fragments (local out tile j % EOTL, k tile j / EOTL + 8 l).
 struct SE0Head {
   int base;
   __device__ int operator()(int j, int l) const {
-    return base + (((j % 2) * 16 + j / 2 + 8 * l) * 64) * 16;
+    return base + (((j % EOTL) * 16 + j / EOTL + 8 * l) * 64) * 16;
   }
 };
 __device__ __forceinline__ SE0Head se0_head(int w) {
@@ -119,8 +155,8 @@ __device__ __forceinline__ SE0Head se0_head(int w) {
 }
 
 struct SplitCarry {
-  f32x4 sg3[8];   // σ10 of generator[-2], local tiles 0, 1
-  f32x4 g4w[2];   // generator[-1].weight rows of local tiles 0, 1
+  f32x4 sg3[8];       // σ10 of generator[-2], local tiles
+  f32x4 g4w[G3OTL];   // generator[-1].weight rows of the local tiles
 };
 
 // Split forward pass (NN.out, :215-259).  X is the full bank; returns τ (same in all waves).
@@ -136,11 +172,11 @@ __device__ __forceinline__ float split_forward(Ring& ring, const float* __restri
   const float cm = compat ? 1.f : 0.f;
   f32x4 L[16], R[16];
 
-  // ---- encoder[0] on Fourier features (:186-190, :227): local out tiles ol = 0, 1 of both
+  // ---- encoder[0] on Fourier features (:186-190, :227): local out tiles ol < EOTL of both
   // columns; every wave computes all 256 features (they are its B operand).
-  f32x4 eb[2];
+  f32x4 eb[EOTL];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) L[i] = zero4();
+  for (int i = 0; i < 2 * EOTL; ++i) L[i] = zero4();
   {
     f32x4 sn[2], cs[2];
     f32x4 bw[2][DIM];
@@ -148,20 +184,15 @@ __device__ __forceinline__ float split_forward(Ring& ring, const float* __restri
     for (int d = 0; d < DIM; ++d) bw[0][d] = ld4(io.Bw + d * H + 4 * g);
     const int e0 = F + OFF_E0 * 4 + wofs<8, 16>(w);
     const int we = F + OFF_EBLK * 4 + wofs<8, 8>(w);
-    run_steps<16, 2, 2, SITE_FWD_E0>(
+    run_steps<8 * EOTL, 2, 2, SITE_FWD_E0>(
         ring, W, lane * 16, SE0Head{e0}, Head<8, 2>{we},
         [&](auto st, const f32x4 (&a)[2]) {
           constexpr int S = decltype(st)::value;
-          constexpr int kt = S / 2, ol = S % 2;
+          constexpr int kt = S / EOTL, ol = S % EOTL;
           if constexpr (S == 1) {
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
-              eb[t] = bload(W, g * 16, BB + (B_E0 + 16 * (2 * w + t)) * 4);
-          }
-          if constexpr (ol == 1 && kt < 7) {
-#pragma unroll
-            for (int d = 0; d < DIM; ++d)
-              bw[(kt + 1) & 1][d] = ld4(io.Bw + d * H + 16 * (kt + 1) + 4 * g);
+            for (int t = 0; t < EOTL; ++t)
+              eb[t] = bload(W, g * 16, BB + (B_E0 + 16 * (EOTL * w + t)) * 4);
           }
           if constexpr (ol == 0) {
 #pragma unroll
@@ -177,12 +208,18 @@ __device__ __forceinline__ float split_forward(Ring& ring, const float* __restri
                 cs[c][s] = x1;
               }
           }
+          // the next Fourier tile's B rows (after this tile's projections)
+          if constexpr (ol == EOTL - 1 && kt < 7) {
+#pragma unroll
+            for (int d = 0; d < DIM; ++d)
+              bw[(kt + 1) & 1][d] = ld4(io.Bw + d * H + 16 * (kt + 1) + 4 * g);
+          }
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
 #pragma unroll
-            for (int c = 0; c < 2; ++c) L[c * 2 + ol] = mfma(a[0][s], sn[c][s], L[c * 2 + ol]);
+            for (int c = 0; c < 2; ++c) L[c * EOTL + ol] = mfma(a[0][s], sn[c][s], L[c * EOTL + ol]);
 #pragma unroll
-            for (int c = 0; c < 2; ++c) L[c * 2 + ol] = mfma(a[1][s], cs[c][s], L[c * 2 + ol]);
+            for (int c = 0; c < 2; ++c) L[c * EOTL + ol] = mfma(a[1][s], cs[c][s], L[c * EOTL + ol]);
           }
         });
   }
@@ -190,8 +227,8 @@ __device__ __forceinline__ float split_forward(Ring& ring, const float* __restri
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int t = c * 2 + i;
+    for (int i = 0; i < EOTL; ++i) {
+      const int t = c * EOTL + i;
       f32x4 s, sg;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -202,48 +239,55 @@ __device__ __forceinline__ float split_forward(Ring& ring, const float* __restri
       L[t] = s;
       if (GRAD) store_tile(sc, T_E0 + t, lane, sg);
     }
-  exchange<2, 2>(sp, 0, L, X);
+  exchange<EOTL, 2>(sp, 0, L, X);
+  PNTF_DUMPX(0)
 
   // ---- encoder residual blocks (:228-232)
-  const int BE = BB + B_EBLK * 4 + w * 2 * 16 * 4;
+  const int BE = BB + B_EBLK * 4 + w * EOTL * 16 * 4;
   const int WE = F + OFF_EBLK * 4 + wofs<8, 8>(w);
   {
-    slice<2, 2>(X, w, R);
-    FwdAct<2, 8, 2, false, GRAD> a0{W, BE, L, sc, T_EBLK, lane, cy.sg3};
-    layer<2, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE, X, lane, a0, NoPre{},
-                                        Head<8, 2>{WE + SZ_E * 4});
+    slice<EOTL, 2>(X, w, R);
+    FwdAct<EOTL, 8, 2, false, GRAD> a0{W, BE, L, sc, T_EBLK, lane, cy.sg3};
+    layer<EOTL, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE, X, lane, a0, NoPre{},
+                                           Head<8, 2>{WE + SZ_E * 4});
     flush(a0);
-    exchange<2, 2>(sp, 1, L, X);
+    exchange<EOTL, 2>(sp, 1, L, X);
+    PNTF_DUMPX(1)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) L[i] = R[i];
-    FwdAct<2, 8, 2, true, GRAD> b0{W, BE + 128 * 4, L, sc, T_EBLK + 16, lane, cy.sg3};
-    layer<2, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + SZ_E * 4, X, lane, b0, NoPre{},
-                                        Head<8, 2>{WE + 2 * SZ_E * 4});
+    for (int i = 0; i < 2 * EOTL; ++i) L[i] = R[i];
+    FwdAct<EOTL, 8, 2, true, GRAD> b0{W, BE + 128 * 4, L, sc, T_EBLK + 16, lane, cy.sg3};
+    layer<EOTL, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + SZ_E * 4, X, lane, b0, NoPre{},
+                                           Head<8, 2>{WE + 2 * SZ_E * 4});
     flush(b0);
-    exchange<2, 2>(sp, 0, L, X);
+    exchange<EOTL, 2>(sp, 0, L, X);
+    PNTF_DUMPX(2)
   }
   {
-    slice<2, 2>(X, w, R);
-    FwdAct<2, 8, 2, false, GRAD> a1{W, BE + 256 * 4, L, sc, T_EBLK + 32, lane, cy.sg3};
-    layer<2, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
-                                        Head<8, 2>{WE + 3 * SZ_E * 4});
+    slice<EOTL, 2>(X, w, R);
+    FwdAct<EOTL, 8, 2, false, GRAD> a1{W, BE + 256 * 4, L, sc, T_EBLK + 32, lane, cy.sg3};
+    layer<EOTL, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
+                                           Head<8, 2>{WE + 3 * SZ_E * 4});
     flush(a1);
-    exchange<2, 2>(sp, 1, L, X);
+    exchange<EOTL, 2>(sp, 1, L, X);
+    PNTF_DUMPX(3)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) L[i] = R[i];
-    FwdAct<2, 8, 2, true, GRAD> b1{W, BE + 384 * 4, L, sc, T_EBLK + 48, lane, cy.sg3};
-    layer<2, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, X, lane, b1, NoPre{},
-                                        Head<8, 2>{F + OFF_E3 * 4 + wofs<8, 8>(w)});
+    for (int i = 0; i < 2 * EOTL; ++i) L[i] = R[i];
+    FwdAct<EOTL, 8, 2, true, GRAD> b1{W, BE + 384 * 4, L, sc, T_EBLK + 48, lane, cy.sg3};
+    layer<EOTL, 8, 2, 2, SITE_FWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, X, lane, b1, NoPre{},
+                                           Head<8, 2>{F + OFF_E3 * 4 + wofs<8, 8>(w)});
     flush(b1);
-    exchange<2, 2>(sp, 0, L, X);
+    exchange<EOTL, 2>(sp, 0, L, X);
+    PNTF_DUMPX(4)
   }
   // ---- encoder[-1] (:234) -> X = [zs | zg]
   {
-    FwdLin<2, 8, 2> e3{W, BB + (B_E3 + 2 * 16 * w) * 4, L, lane};
-    layer<2, 8, 2, 2, SITE_FWD_ENC, 4>(ring, W, F + OFF_E3 * 4 + wofs<8, 8>(w), X, lane, e3,
-                                        NoPre{}, Head<16>{F + OFF_GBLK * 4 + wofs<16, 16>(w)});
+    FwdLin<EOTL, 8, 2> e3{W, BB + (B_E3 + EOTL * 16 * w) * 4, L, lane};
+    layer<EOTL, 8, 2, 2, SITE_FWD_ENC, GNL>(ring, W, F + OFF_E3 * 4 + wofs<8, 8>(w), X, lane, e3,
+                                             NoPre{},
+                                             Head<16>{F + OFF_GBLK * 4 + wofs<16, 16>(w)});
     flush(e3);
-    exchange<2, 2>(sp, 1, L, X);
+    exchange<EOTL, 2>(sp, 1, L, X);
+    PNTF_DUMPX(5)
   }
 
   // ---- merge (:236-244), in place and redundantly in every wave: X = u = [M | m]
@@ -271,39 +315,44 @@ __device__ __forceinline__ float split_forward(Ring& ring, const float* __restri
     const int wb = opaque(F + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4 + wofs<16, 16>(w));
     const int wn = opaque(i < 2 ? F + (OFF_GBLK + (2 * i + 2) * SZ_G) * 4 + wofs<16, 16>(w)
                                 : F + OFF_G3 * 4 + wofs<8, 16>(w));
-    const int bg = BB + (B_GBLK + (2 * i) * 256 + 4 * 16 * w) * 4;
-    slice<4, 1>(X, w, R);
-    FwdAct<4, 16, 1, false, GRAD> ga{W, bg, L, sc, T_GBLK + 32 * i, lane, cy.sg3};
-    layer<4, 16, 1, 1, SITE_FWD_GEN, 4>(ring, W, wa, X, lane, ga, NoPre{}, Head<16>{wb});
+    const int bg = BB + (B_GBLK + (2 * i) * 256 + GOTL * 16 * w) * 4;
+    slice<GOTL, 1>(X, w, R);
+    FwdAct<GOTL, 16, 1, false, GRAD> ga{W, bg, L, sc, T_GBLK + 32 * i, lane, cy.sg3};
+    layer<GOTL, 16, 1, 1, SITE_FWD_GEN, GNL>(ring, W, wa, X, lane, ga, NoPre{}, Head<16>{wb});
     flush(ga);
-    exchange<4, 1>(sp, 0, L, X);
+    exchange<GOTL, 1>(sp, 0, L, X);
+    PNTF_DUMPX(6)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) L[t] = R[t];
-    FwdAct<4, 16, 1, true, GRAD> gb{W, bg + 256 * 4, L, sc, T_GBLK + 32 * i + 16, lane, cy.sg3};
-    // the last block hands over to generator[-2], 2 local out tiles per step
+    for (int t = 0; t < GOTL; ++t) L[t] = R[t];
+    FwdAct<GOTL, 16, 1, true, GRAD> gb{W, bg + 256 * 4, L, sc, T_GBLK + 32 * i + 16, lane,
+                                       cy.sg3};
+    // the last block hands over to generator[-2] (G3OTL local out tiles per step)
     if (i < 2)
-      layer<4, 16, 1, 1, SITE_FWD_GEN, 4>(ring, W, wb, X, lane, gb, NoPre{}, Head<16>{wn});
+      layer<GOTL, 16, 1, 1, SITE_FWD_GEN, GNL>(ring, W, wb, X, lane, gb, NoPre{}, Head<16>{wn});
     else
-      layer<4, 16, 1, 1, SITE_FWD_GEN, 2>(ring, W, wb, X, lane, gb, NoPre{}, Head<16>{wn});
+      layer<GOTL, 16, 1, 1, SITE_FWD_GEN, G3OTL>(ring, W, wb, X, lane, gb, NoPre{},
+                                                  Head<16>{wn});
     flush(gb);
-    exchange<4, 1>(sp, 1, L, X);
+    exchange<GOTL, 1>(sp, 1, L, X);
+    PNTF_DUMPX(7)
   }
 
-  // ---- generator[-2] + act (:251-252): local tiles L[0..1], σ kept for the reverse sweep
+  // ---- generator[-2] + act (:251-252): local tiles L[0..G3OTL), σ kept for the reverse sweep
 #pragma unroll
-  for (int t = 0; t < 2; ++t) cy.g4w[t] = bload(W, g * 16, BB + (B_G4W + 16 * (2 * w + t)) * 4);
+  for (int t = 0; t < G3OTL; ++t)
+    cy.g4w[t] = bload(W, g * 16, BB + (B_G4W + 16 * (G3OTL * w + t)) * 4);
   const float g4b = bload(W, 0, BB + B_G4B * 4)[0];
   {
-    FwdAct<2, 16, 1, false, GRAD, GRAD> g3{W, BB + (B_G3 + 2 * 16 * w) * 4, L, sc, T_G3, lane,
-                                           cy.sg3};
-    layer<2, 16, 1, 1, SITE_FWD_GEN, NLA>(ring, W, F + OFF_G3 * 4 + wofs<8, 16>(w), X, lane, g3,
-                                          NoPre{}, after);
+    FwdAct<G3OTL, 16, 1, false, GRAD, GRAD> g3{W, BB + (B_G3 + G3OTL * 16 * w) * 4, L, sc, T_G3,
+                                               lane, cy.sg3};
+    layer<G3OTL, 16, 1, 1, SITE_FWD_GEN, NLA>(ring, W, F + OFF_G3 * 4 + wofs<8, 16>(w), X, lane,
+                                               g3, NoPre{}, after);
     flush(g3);
   }
   // ---- head (:254-255): partial dot of the local tiles, summed over the waves
   float part[1] = {0.f};
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < G3OTL; ++t)
 #pragma unroll
     for (int s = 0; s < 4; ++s) part[0] = fmaf(cy.g4w[t][s], L[t][s], part[0]);
   part[0] += __shfl_xor(part[0], 16);
@@ -329,110 +378,128 @@ __device__ __forceinline__ void split_backward(Ring& ring, const float* __restri
   // ---- head and generator[-2] (:592-613): dv = d · G4 ⊙ σ10(y3), local tiles -> X[0..7]
   const float dd = 0.1f * tau * (1.f - tau);
 #pragma unroll
-  for (int t = 0; t < 2; ++t) L[t] = (dd * cy.g4w[t]) * cy.sg3[t];
-  exchange<2, 1>(sp, 0, L, X);
+  for (int t = 0; t < G3OTL; ++t) L[t] = (dd * cy.g4w[t]) * cy.sg3[t];
+  exchange<G3OTL, 1>(sp, 0, L, X);
+  PNTF_DUMPX(20)
   // du = G3^T dv ⊙ σ10(y2 of generator block 2)   (G3^T: 256 x 128, OT 16, KT 8)
   {
-    Bwd<4, 8, 1, false, true> l{L, sc, T_GBLK + 32 * 2 + 16, lane};
-    layer<4, 8, 1, 1, SITE_BWD_GEN, 4>(ring, W, Bk + OFF_G3 * 4 + wofs<16, 8>(w), X, lane, l,
-                                       NoPre{},
-                                       Head<16>{Bk + (OFF_GBLK + 5 * SZ_G) * 4 + wofs<16, 16>(w)});
+    Bwd<GOTL, 8, 1, false, true> l{L, sc, T_GBLK + 32 * 2 + 16, lane};
+    layer<GOTL, 8, 1, 1, SITE_BWD_GEN, GNL>(
+        ring, W, Bk + OFF_G3 * 4 + wofs<16, 8>(w), X, lane, l, NoPre{},
+        Head<16>{Bk + (OFF_GBLK + 5 * SZ_G) * 4 + wofs<16, 16>(w)});
     flush(l);
-    exchange<4, 1>(sp, 1, L, X);
+    exchange<GOTL, 1>(sp, 1, L, X);
+    PNTF_DUMPX(21)
   }
   // ---- generator blocks, reverse (:615-618)
 #pragma unroll 1
   for (int i = 2; i >= 0; --i) {
     const int wa = opaque(Bk + (OFF_GBLK + (2 * i) * SZ_G) * 4 + wofs<16, 16>(w));
     const int wb = opaque(Bk + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4 + wofs<16, 16>(w));
-    slice<4, 1>(X, w, R);   // dr
-    Bwd<4, 16, 1, false, true> lb{L, sc, T_GBLK + 32 * i, lane};
-    layer<4, 16, 1, 1, SITE_BWD_GEN, 4>(ring, W, wb, X, lane, lb, NoPre{}, Head<16>{wa});
+    slice<GOTL, 1>(X, w, R);   // dr
+    Bwd<GOTL, 16, 1, false, true> lb{L, sc, T_GBLK + 32 * i, lane};
+    layer<GOTL, 16, 1, 1, SITE_BWD_GEN, GNL>(ring, W, wb, X, lane, lb, NoPre{}, Head<16>{wa});
     flush(lb);
-    exchange<4, 1>(sp, 0, L, X);
+    exchange<GOTL, 1>(sp, 0, L, X);
+    PNTF_DUMPX(22)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) L[t] = R[t];
+    for (int t = 0; t < GOTL; ++t) L[t] = R[t];
     if (i > 0) {
       const int wn = opaque(Bk + (OFF_GBLK + (2 * i - 1) * SZ_G) * 4 + wofs<16, 16>(w));
-      Bwd<4, 16, 1, true, true> la{L, sc, T_GBLK + 32 * (i - 1) + 16, lane};
-      layer<4, 16, 1, 1, SITE_BWD_GEN, 4>(ring, W, wa, X, lane, la, NoPre{}, Head<16>{wn});
+      Bwd<GOTL, 16, 1, true, true> la{L, sc, T_GBLK + 32 * (i - 1) + 16, lane};
+      layer<GOTL, 16, 1, 1, SITE_BWD_GEN, GNL>(ring, W, wa, X, lane, la, NoPre{}, Head<16>{wn});
       flush(la);
     } else {
-      Bwd<4, 16, 1, true, false> la{L, sc, 0, lane};
-      layer<4, 16, 1, 1, SITE_BWD_GEN, 2>(ring, W, wa, X, lane, la, NoPre{},
-                                          Head<8, 2>{Bk + OFF_E3 * 4 + wofs<8, 8>(w)});
+      Bwd<GOTL, 16, 1, true, false> la{L, sc, 0, lane};
+      layer<GOTL, 16, 1, 1, SITE_BWD_GEN, 2>(ring, W, wa, X, lane, la, NoPre{},
+                                             Head<8, 2>{Bk + OFF_E3 * 4 + wofs<8, 8>(w)});
       flush(la);
     }
-    exchange<4, 1>(sp, 1, L, X);
+    exchange<GOTL, 1>(sp, 1, L, X);
+    PNTF_DUMPX(23)
   }
   // ---- merge Jacobian (:620-627), redundantly in every wave: X = [dzs | dzg]
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     f32x4 s0 = load_tile(sc, T_S0 + t, lane);
+    PNTF_DUMPT(30, t, s0)
     f32x4 s1 = 1.f - s0;
     f32x4 dM = X[t], dm = X[8 + t];
     X[t] = s0 * dM + s1 * dm;
     X[8 + t] = s1 * dM + s0 * dm;
   }
+#ifdef PNTF_DIAG_MERGENOP   // diagnostics only (tests/diag split variants)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#endif
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1)
   const int WE = Bk + OFF_EBLK * 4 + wofs<8, 8>(w);
   {
-    Bwd<2, 8, 2, false, true> e3{L, sc, T_EBLK + 32 * 1 + 16, lane};
-    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, Bk + OFF_E3 * 4 + wofs<8, 8>(w), X, lane, e3,
-                                       NoPre{}, Head<8, 2>{WE + 3 * SZ_E * 4});
+    Bwd<EOTL, 8, 2, false, true> e3{L, sc, T_EBLK + 32 * 1 + 16, lane};
+    layer<EOTL, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, Bk + OFF_E3 * 4 + wofs<8, 8>(w), X, lane, e3,
+                                           NoPre{}, Head<8, 2>{WE + 3 * SZ_E * 4});
     flush(e3);
-    exchange<2, 2>(sp, 0, L, X);
+#ifdef PNTF_DEBUG_DUMP
+    for (int i_ = 0; i_ < 2 * EOTL; ++i_) { PNTF_DUMPW(40, i_, L[i_]) }
+#endif
+    exchange<EOTL, 2>(sp, 0, L, X);
+    PNTF_DUMPX(24)
   }
   // ---- encoder blocks, reverse (:633-636)
   {
-    slice<2, 2>(X, w, R);
-    Bwd<2, 8, 2, false, true> b1{L, sc, T_EBLK + 32, lane};
-    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, X, lane, b1, NoPre{},
-                                       Head<8, 2>{WE + 2 * SZ_E * 4});
+    slice<EOTL, 2>(X, w, R);
+    Bwd<EOTL, 8, 2, false, true> b1{L, sc, T_EBLK + 32, lane};
+    layer<EOTL, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 3 * SZ_E * 4, X, lane, b1, NoPre{},
+                                           Head<8, 2>{WE + 2 * SZ_E * 4});
     flush(b1);
-    exchange<2, 2>(sp, 1, L, X);
+    exchange<EOTL, 2>(sp, 1, L, X);
+    PNTF_DUMPX(25)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) L[i] = R[i];
-    Bwd<2, 8, 2, true, true> a1{L, sc, T_EBLK + 16, lane};
-    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
-                                       Head<8, 2>{WE + 1 * SZ_E * 4});
+    for (int i = 0; i < 2 * EOTL; ++i) L[i] = R[i];
+    Bwd<EOTL, 8, 2, true, true> a1{L, sc, T_EBLK + 16, lane};
+    layer<EOTL, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
+                                           Head<8, 2>{WE + 1 * SZ_E * 4});
     flush(a1);
-    exchange<2, 2>(sp, 0, L, X);
+    exchange<EOTL, 2>(sp, 0, L, X);
+    PNTF_DUMPX(26)
   }
-  const int E0T = Bk + OFF_E0 * 4 + wofs<16, 8>(w) / 2;   // local feature tiles 2w, 2w + 1
+  // local Fourier feature tiles kf = FKL·w + kl of the fold (sin rows kf, cos rows kf + 8)
+  const int E0T = Bk + OFF_E0 * 4 + FKL * w * 8 * 1024;
   {
-    slice<2, 2>(X, w, R);
-    Bwd<2, 8, 2, false, true> b0{L, sc, T_EBLK, lane};
-    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 1 * SZ_E * 4, X, lane, b0, NoPre{},
-                                       Head<8, 2>{WE});
+    slice<EOTL, 2>(X, w, R);
+    Bwd<EOTL, 8, 2, false, true> b0{L, sc, T_EBLK, lane};
+    layer<EOTL, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE + 1 * SZ_E * 4, X, lane, b0, NoPre{},
+                                           Head<8, 2>{WE});
     flush(b0);
-    exchange<2, 2>(sp, 1, L, X);
+    exchange<EOTL, 2>(sp, 1, L, X);
+    PNTF_DUMPX(27)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) L[i] = R[i];
-    Bwd<2, 8, 2, true, true> a0{L, sc, T_E0, lane};
-    layer<2, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE, X, lane, a0, NoPre{},
-                                       [=](int j, int l) {
-                                         return E0T + ((j / 8 + 8 * l) * 8 + j % 8) * 1024;
-                                       });
+    for (int i = 0; i < 2 * EOTL; ++i) L[i] = R[i];
+    Bwd<EOTL, 8, 2, true, true> a0{L, sc, T_E0, lane};
+    layer<EOTL, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, WE, X, lane, a0, NoPre{},
+                                           [=](int j, int l) {
+                                             return E0T + ((j / 8 + 8 * l) * 8 + j % 8) * 1024;
+                                           });
     flush(a0);
-    exchange<2, 2>(sp, 0, L, X);
+    exchange<EOTL, 2>(sp, 0, L, X);
+    PNTF_DUMPX(28)
   }
 
-  // ---- encoder[0]^T fused with the Fourier Jacobian (:639-645): this wave's feature tiles
-  // kf = 2w + kl (sin rows kf, cos rows kf + 8), then the dim-vector summed over the waves.
-  f32x4 ph[2][2][2];   // [kl][sin|cos rows][column]
+  // ---- encoder[0]^T fused with the Fourier Jacobian (:639-645): this wave's feature tiles,
+  // then the dim-vector summed over the waves.
+  f32x4 ph[FKL][2][2];   // [kl][sin|cos rows][column]
 #pragma unroll
-  for (int kl = 0; kl < 2; ++kl)
+  for (int kl = 0; kl < FKL; ++kl)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int c = 0; c < 2; ++c) ph[kl][u][c] = zero4();
-  f32x4 bw[2][DIM];
+  f32x4 bw[FKL][DIM];
 #pragma unroll
-  for (int kl = 0; kl < 2; ++kl)
+  for (int kl = 0; kl < FKL; ++kl)
 #pragma unroll
-    for (int d = 0; d < DIM; ++d) bw[kl][d] = ld4(io.Bw + d * H + 16 * (2 * w + kl) + 4 * g);
-  run_steps<16, 2, NLA, SITE_FOLD>(
+    for (int d = 0; d < DIM; ++d)
+      bw[kl][d] = ld4(io.Bw + d * H + 16 * (FKL * w + kl) + 4 * g);
+  run_steps<8 * FKL, 2, NLA, SITE_FOLD>(
       ring, W, lane * 16,
       [&](int st, int l) { return E0T + ((st / 8 + 8 * l) * 8 + st % 8) * 1024; }, after,
       [&](auto st, const f32x4 (&a)[2]) {
@@ -450,7 +517,7 @@ __device__ __forceinline__ void split_backward(Ring& ring, const float* __restri
 #pragma unroll
   for (int j = 0; j < 2 * DIM; ++j) acc[j] = 0.f;
 #pragma unroll
-  for (int kl = 0; kl < 2; ++kl)
+  for (int kl = 0; kl < FKL; ++kl)
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -460,6 +527,9 @@ __device__ __forceinline__ void split_backward(Ring& ring, const float* __restri
         for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], TWO_PI * bw[kl][d][s], q);
         float sn, cs;
         sincos_fast(q, sn, cs);
+#ifdef PNTF_DIAG_FOLDNOP   // diagnostics only (tests/diag split variants)
+        asm volatile("s_nop 7\n\ts_nop 7" : "+v"(sn), "+v"(cs));
+#endif
         float gg = ph[kl][0][c][s] * cs - ph[kl][1][c][s] * sn;
 #pragma unroll
         for (int d = 0; d < DIM; ++d) acc[c * DIM + d] = fmaf(TWO_PI * bw[kl][d][s], gg, acc[c * DIM + d]);
@@ -480,7 +550,7 @@ __device__ __forceinline__ void split_backward(Ring& ring, const float* __restri
 // τ / ∇τ / epilogues on split tiles for small batches: one workgroup per 16-pair tile
 // (grid-stride), same outputs as field_kernel<DIM, KIND>.
 template <int DIM, int KIND>
-__global__ __launch_bounds__(256, 1) void field_split_kernel(FieldArgs a) {
+__global__ __launch_bounds__(64 * SPLIT, 1) void field_split_kernel(FieldArgs a) {
   constexpr bool GRAD = KIND != K_TAU && KIND != K_TRAVEL;
   __shared__ float smem[SPLIT_LDS_FLOATS];
   const int lane = threadIdx.x & 63;
@@ -491,7 +561,7 @@ __global__ __launch_bounds__(256, 1) void field_split_kernel(FieldArgs a) {
       GRAD ? a.ws + ((int64_t)blockIdx.x * SPLIT + w) * SCRATCH_FLOATS_PER_WAVE : nullptr);
   const Rsrc W = make_rsrc(a.P, PACKED_FLOATS * 4);
   const SE0Head e0h = se0_head(w);
-  const Head<8> g3h{(OFF_BWD + OFF_G3) * 4 + wofs<16, 8>(w)};
+  const Head<8> g3h{(OFF_BWD + OFF_G3) * 4 + wofs<16, 8>(w)};   // G3^T local out tiles
   Ring ring;
   ring_fill<2>(ring, W, lane * 16, e0h);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -503,7 +573,7 @@ __global__ __launch_bounds__(256, 1) void field_split_kernel(FieldArgs a) {
     float tau;
     float ds[DIM], dg[DIM];
     if constexpr (GRAD) {
-      tau = split_forward<DIM, true, 4>(ring, a.P, io, X, cy, sc, a.compat, sp, g3h);
+      tau = split_forward<DIM, true, GNL>(ring, a.P, io, X, cy, sc, a.compat, sp, g3h);
       drain_stores();
       split_backward<DIM, 2>(ring, a.P, io, tau, X, cy, sc, sp, ds, dg, e0h);
     } else {
@@ -518,7 +588,7 @@ __global__ __launch_bounds__(256, 1) void field_split_kernel(FieldArgs a) {
 // plan_kernel (test/gib_plan.py:74-86, test/arm_plan.py:140-152) with per-query freeze.
 // ws holds one scratch slot per wave (4 per workgroup).
 template <int DIM>
-__global__ __launch_bounds__(256, 1) void plan_split_kernel(PlanArgs a) {
+__global__ __launch_bounds__(64 * SPLIT, 1) void plan_split_kernel(PlanArgs a) {
   __shared__ float smem[SPLIT_LDS_FLOATS];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -529,7 +599,7 @@ __global__ __launch_bounds__(256, 1) void plan_split_kernel(PlanArgs a) {
   const int cap = a.max_iter + 1;
   const int64_t rows = (int64_t)cap + 1;
   const SE0Head e0h = se0_head(w);
-  const Head<8> g3h{(OFF_BWD + OFF_G3) * 4 + wofs<16, 8>(w)};
+  const Head<8> g3h{(OFF_BWD + OFF_G3) * 4 + wofs<16, 8>(w)};   // G3^T local out tiles
   Ring ring;
   ring_fill<2>(ring, W, lane * 16, e0h);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -560,7 +630,7 @@ __global__ __launch_bounds__(256, 1) void plan_split_kernel(PlanArgs a) {
     int it = 0;
     for (; it < cap; ++it) {
       if (!__any(active)) break;
-      float tau = split_forward<DIM, true, 4>(ring, a.P, io, X, cy, sc, a.compat, sp, g3h);
+      float tau = split_forward<DIM, true, GNL>(ring, a.P, io, X, cy, sc, a.compat, sp, g3h);
       drain_stores();
       float ds[DIM], dg[DIM], vs[DIM], vg[DIM];
       split_backward<DIM, 2>(ring, a.P, io, tau, X, cy, sc, sp, ds, dg, e0h);

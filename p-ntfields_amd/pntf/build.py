@@ -44,7 +44,8 @@ PACKED_FP32 = re.compile(r"\bv_pk_(mul|add|fma)_f32\b")
 SCRATCH_STORE = re.compile(r"buffer_store_dwordx4 v\[\d+:\d+\], v\d+, (s\[\d+:\d+\])[^\n]*\bnt\b")
 BUFFER_LOAD = re.compile(r"buffer_load_dwordx4 v\[\d+:\d+\], v\d+, (s\[\d+:\d+\])([^\n]*)")
 # units whose kernels keep a saved-σ scratch slot (τ-only / travel-time kernels have none)
-SCRATCH_UNITS = re.compile(r"^(field_d\d_k[123]|fsplit_d\d_k[123]|wide_d\d_k[123]|plan_.*|residual_d\d)$")
+SCRATCH_UNITS = re.compile(r"^(field_d\d_k[123]|fsplit_d\d_k[123]|wide_d\d_k[123]|plan_d\d|plan_split_d\d|"
+                           r"residual_d\d)$")
 
 
 def scratch_policy_violations(asm):
@@ -62,6 +63,10 @@ def scratch_policy_violations(asm):
                 bad += 1
     return descs, good, bad
 
+# units whose kernels must not spill SGPRs either: the headline τ+∇τ kernel and its τ-only /
+# travel-time siblings (the narrow 16-pair kernels still spill ~24-335 SGPRs to VGPR lanes)
+SGPR_SPILL_FREE = re.compile(r"^wide_d\d_k[014]$")
+
 UNITS = (
     [("field_d%d_k%d" % (d, k), "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k])
      for d in (3, 6) for k in range(5)]
@@ -78,6 +83,12 @@ UNITS = (
     + [("plan_d3", "pntf_kernels.hip", ["-DPNTF_DIM=3", "-DPNTF_PLAN"]),
        ("plan_d6", "pntf_kernels.hip", ["-DPNTF_DIM=6", "-DPNTF_PLAN", "-DPNTF_PF_STEPS=2"])]
     + [("plan_split_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_SPLIT"])
+       for d in (3, 6)]
+    # quad kernels (pntf_quad.h): 4-pair tiles, σ10 in LDS (no scratch slot)
+    + [("quad_d%d_k%d" % (d, k), "pntf_kernels.hip",
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_QUAD_FIELD"])
+       for d in (3, 6) for k in range(5)]
+    + [("plan_quad_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD"])
        for d in (3, 6)]
     + [("residual_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_RESIDUAL"])
        for d in (3, 6)]
@@ -157,6 +168,10 @@ def _compile(unit):
         v.get("VGPRs Spill", 0) and not name.startswith("wide_"))}
     if bad:
         raise RuntimeError("VGPR spills / scratch in %s: %s" % (name, bad))
+    if SGPR_SPILL_FREE.match(name):
+        sbad = {k: v["SGPRs Spill"] for k, v in res.items() if v.get("SGPRs Spill", 0)}
+        if sbad:
+            raise RuntimeError("SGPR spills in %s (must stay spill-free): %s" % (name, sbad))
     for asm in glob.glob(os.path.join(d, "*amdgcn*gfx950*.s")):
         with open(asm) as fh:
             m = PACKED_FP32.search(fh.read())

@@ -101,7 +101,7 @@ def _prep(xp, Btab, env, dim):
     return xp, Bt, env
 
 
-SCHEDULES = {"auto": 0, "wave_tile": 1, "split_tile": 2, "wide_tile": 3}
+SCHEDULES = {"auto": 0, "wave_tile": 1, "split_tile": 2, "wide_tile": 3, "quad_tile": 4}
 FIELD_TAU, FIELD_TAU_GRAD, FIELD_VELOCITY, FIELD_SPEED, FIELD_TRAVEL = range(5)
 
 

@@ -3,9 +3,23 @@
 // tests/diag/build_perf.sh into tests/diag/libperf_<name>.so and timed by perf_variants.py.
 #ifdef PERF_WIDE
 #include "pntf_wide.h"
+#elif defined(PERF_SPLIT)
+#include "pntf_split.h"
+#elif defined(PERF_QUAD)
+#include "pntf_quad.h"
 #else
 #include "pntf_field.h"
 #endif
+
+extern "C" int perf_split_width() {
+#ifdef PERF_QUAD
+  return -4;   // quad tiles: 4 pairs per workgroup
+#elif defined(PERF_SPLIT)
+  return pntf::SPLIT;
+#else
+  return 0;
+#endif
+}
 
 extern "C" int perf_tau_grad(int grid, const float* P, const float* xp, int64_t n,
                              const float* Btab, float* tau, float* dtau, float* ws,
@@ -14,6 +28,11 @@ extern "C" int perf_tau_grad(int grid, const float* P, const float* xp, int64_t 
   FieldArgs a{P, xp, Btab, nullptr, n, 1, 0, tau, dtau, ws};
 #ifdef PERF_WIDE
   hipLaunchKernelGGL((wide_field_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(256), 0, stream, a);
+#elif defined(PERF_QUAD)    // one workgroup per 4-pair tile
+  hipLaunchKernelGGL((field_quad_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(256), 0, stream, a);
+#elif defined(PERF_SPLIT)   // one workgroup per 16-pair tile; ws: SPLIT slots per workgroup
+  hipLaunchKernelGGL((field_split_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(64 * SPLIT), 0,
+                     stream, a);
 #else
   hipLaunchKernelGGL((field_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(256), 0, stream, a);
 #endif

@@ -50,7 +50,10 @@ def test_pure_queries_without_gpu(lib):
     mats = 128 * 256 + 4 * 128 * 128 + 128 * 128 + 6 * 256 * 256 + 128 * 256
     plain = 128 + 4 * 128 + 128 + 6 * 256 + 128 + 128 + 4
     wide = 2 * mats + 19 * 256 + 16 * 256 + 4
-    assert lib.pntf_packed_floats() == 2 * mats + plain + wide
+    # then (64-float aligned) the quad streams: both directions once more, and per wave 14
+    # bias / head fragments
+    off_quad = (2 * mats + plain + wide + 63) // 64 * 64
+    assert lib.pntf_packed_floats() == off_quad + 2 * mats + 4 * 14 * 256
     lib.pntf_status_string.restype = ctypes.c_char_p
     assert lib.pntf_status_string(1) == b"invalid argument"
 
@@ -168,6 +171,51 @@ def test_wide_pack_layout_feeds_32x32x2_fragments():
         assert frag[ot, kt, u, 32 * h + i, s] == W[32 * ot + i, 32 * kt + row(r, h)]
 
 
+def _pack_quad_numpy(W, dir_):
+    """Restatement of pack_quad_kernel (pntf_quad.h): the 4 wave streams of one layer,
+    shape (wave, groups, IN/16, 64 lanes, 4)."""
+    A = W.T if dir_ else W
+    OUT, IN = A.shape
+    w, g, q, lane, e = np.meshgrid(np.arange(4), np.arange(OUT // 64), np.arange(IN // 16),
+                                   np.arange(64), np.arange(4), indexing="ij")
+    row = w * (OUT // 4) + 16 * g + 4 * (lane >> 4) + (lane & 3)
+    k = 16 * q + 4 * e + ((lane >> 2) & 3)
+    return A[row, k]
+
+
+def test_quad_pack_feeds_4x4x1_blocks():
+    """Emulate one quad layer on the packed stream: v_mfma_f32_4x4x1_16b_f32 gives lane l
+    D[i] += A(lane 4 (l >> 2) + i) * B(lane l) (block l >> 2, row i, column l & 3; layout
+    measured by tests/diag/quad_probe.hip), B lane l = act[4 s + kb][pair l & 3]; after the
+    sum over the k sub-blocks kb (lanes l ^ 4, l ^ 8) lane (og, kb, j) keeps D[kb] = the
+    layer output at row w·OUT/4 + 16 g + 4 og + kb, pair j."""
+    rng = np.random.default_rng(2)
+    for (rows, cols, dir_) in [(128, 256, 0), (256, 128, 1), (256, 256, 0)]:
+        W = rng.standard_normal((rows, cols)).astype(np.float64)
+        P = _pack_quad_numpy(W, dir_)
+        A = W.T if dir_ else W
+        OUT, IN = A.shape
+        act = rng.standard_normal((IN, 4))
+        ref = A @ act
+        lane = np.arange(64)
+        og, kb, j = lane >> 4, (lane >> 2) & 3, lane & 3
+        for w in range(4):
+            for g in range(OUT // 64):
+                D = np.zeros((64, 4))
+                for q in range(IN // 16):
+                    for e in range(4):
+                        s = 4 * q + e
+                        a = P[w, g, q, :, e]
+                        b = act[4 * s + kb, j]
+                        for i in range(4):
+                            D[:, i] += a[4 * (lane >> 2) + i] * b
+                S = D + D[lane ^ 4]
+                S = S + S[lane ^ 8]
+                v = S[lane, kb]
+                rws = w * (OUT // 4) + 16 * g + 4 * og + kb
+                np.testing.assert_allclose(v, ref[rws, j], rtol=1e-12, atol=1e-9)
+
+
 def test_synth_is_deterministic():
     np.testing.assert_array_equal(synth.make_pairs(100, 3, 2), synth.make_pairs(100, 3, 2))
     x = synth.make_pairs(5000, 3, 2)
@@ -187,7 +235,7 @@ def test_field_ex_validates_kind_and_schedule_without_gpu():
     assert b"schedule" in L.pntf_last_error()
     # empty batch: valid for every kind and schedule, nothing launched
     for kind in range(5):
-        for sched in range(4):
+        for sched in range(5):
             assert L.pntf_field_ex(kind, None, 3, None, 0, None, None, 1, 0, None, None, None, 0,
                                    sched, None) == 0
 

@@ -51,11 +51,11 @@ def packed(W, dev):
     return ops.pack_weights(params)
 
 
-@pytest.fixture(params=["wave_tile", "split_tile", "wide_tile"])
+@pytest.fixture(params=["wave_tile", "split_tile", "wide_tile", "quad_tile"])
 def field_schedule(request):
-    """Run a field test with one wave per 16-pair tile, with split tiles (pntf_split.h) and
-    with one wave per 32-pair tile (pntf_wide.h); the schedule is passed per call
-    (pntf_field_ex), no library state changes."""
+    """Run a field test with one wave per 16-pair tile, with split tiles (pntf_split.h), with
+    one wave per 32-pair tile (pntf_wide.h) and with 4-pair quad tiles (pntf_quad.h); the
+    schedule is passed per call (pntf_field_ex), no library state changes."""
     return request.param
 
 
@@ -156,7 +156,7 @@ def test_coincident_endpoints(packed, dev, W):
     close(d.cpu().numpy(), do)
 
 
-@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile"])
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile", "quad_tile"])
 def test_gibson_planner_vs_reference(packed, dev, schedule):
     p = load("plan_gib.npz")
     path, steps = ops.plan(packed, T(p["starts"], dev), T(p["B"], dev), dim=3, step=0.03,
@@ -170,7 +170,7 @@ def test_gibson_planner_vs_reference(packed, dev, schedule):
     assert np.abs(path[np.arange(len(steps)), steps] - last).max() < 1e-3
 
 
-@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile"])
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile", "quad_tile"])
 def test_arm_planner_vs_reference(packed, dev, schedule):
     p = load("plan_arm.npz")
     path, steps = ops.plan(packed, T(p["starts"], dev), T(p["B"].T, dev), dim=6, step=0.015,
@@ -180,7 +180,7 @@ def test_arm_planner_vs_reference(packed, dev, schedule):
     assert np.abs(path - p["paths"]).max() < 1e-3
 
 
-@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile"])
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile", "quad_tile"])
 def test_planner_batch_vs_oracle(packed, dev, schedule, W):
     q = 37
     xp0 = synth.make_box_pairs(q, 6, seed=77)
@@ -206,6 +206,10 @@ def test_planner_schedules_agree(packed, dev, dim, compat):
     ps, ss = ops.plan(packed, xp0, B, schedule="split_tile", **kw)
     assert torch.equal(sw, ss)
     assert (ps - pw).abs().max().item() < 1e-4
+    # quad tiles (4 queries per workgroup, ~9 tiles per workgroup at this q)
+    pq, sq = ops.plan(packed, xp0, B, schedule="quad_tile", **kw)
+    assert torch.equal(sw, sq)
+    assert (pq - pw).abs().max().item() < 1e-4
 
 
 def test_drop_in_models_api(W, dev):

@@ -18,7 +18,7 @@
 //     column, conflict-free), then one workgroup barrier per layer;
 //   * the saved σ10 values stay in LDS (compact, per wave), so there is no global scratch;
 //   * each wave's weight fragments are packed in consumption order (pntf_common.h Q_LAYERS),
-//     so the prefetch ring is one linear stream of 1 KiB fragments, 8 in flight, that wraps
+//     so the prefetch ring is one linear stream of 1 KiB fragments, 32 in flight, that wraps
 //     from the last reverse layer into the next step's encoder[0].
 // 1024 queries are 256 tiles: every CU of the chip has one.  Reductions whose result every
 // lane consumes (τ, ∇τ) use xor butterflies and a fixed wave order, so all lanes of a pair
@@ -33,10 +33,13 @@ constexpr int QPAIRS = 4;
 #define PNTF_Q_CHAINS 2
 #endif
 constexpr int QCH = PNTF_Q_CHAINS;
+// Fragments in flight per wave: the ∇τ kernels (1056 fragments per step, a multiple of 32)
+// run PNTF_QRING of them; the τ-only kernels wrap every 528 fragments and run 16.
 #ifndef PNTF_QRING
-#define PNTF_QRING 16
+#define PNTF_QRING 32
 #endif
-constexpr int QRING = PNTF_QRING;           // fragments in flight per wave
+constexpr int QRING = PNTF_QRING;
+constexpr int QRING_TAU = 16;
 constexpr int Q_NF_ALL = 2 * Q_NF_FWD;
 constexpr int QBUF = 2 * 16 * 68;           // activation buffer: 2 columns x 16 lane rows x 68
 constexpr int QNSIG = 48;                   // saved σ10 slots per wave (64 floats each)
@@ -101,12 +104,13 @@ struct QCx {
   }
 };
 
+template <int QR>
 struct QRing {
-  f32x4 r[QRING];
+  f32x4 r[QR];
   int next;   // next fragment to load (wave-uniform)
 };
-template <int NF>
-__device__ __forceinline__ void qfetch(QRing& ring, Rsrc W, int lane, int slot) {
+template <int NF, int QR>
+__device__ __forceinline__ void qfetch(QRing<QR>& ring, Rsrc W, int lane, int slot) {
 #ifdef PNTF_QABL_NOLOAD   // diagnostics only (tests/diag timing ablations; wrong results)
   ring.r[slot] = ring.r[slot] * 1.0001f;
 #else
@@ -115,28 +119,23 @@ __device__ __forceinline__ void qfetch(QRing& ring, Rsrc W, int lane, int slot) 
   ring.next = ring.next + 1 == NF ? 0 : ring.next + 1;
 }
 
-// One layer: `groups` groups of 16 out rows; per group IN/16 fragments of 4 k steps x NC
-// columns; B operands read from `in` (IN features, row stride IN/4 + 4).  epi(g, v[NC]) gets
-// the compact sums of group g.
-template <int NC, int IN, int NF, class Epi>
-__device__ __forceinline__ void qlayer(QRing& ring, Rsrc W, const QCx& cx, const lds_f* in,
-                                       int groups, Epi&& epi) {
+// One layer: G groups of 16 out rows; per group IN/16 fragments of 4 k steps x NC columns;
+// B operands read from `in` (IN features, row stride IN/4 + 4).  The layer's first fragment
+// sits in ring slot S0.  epi(g, v[NC]) gets the compact sums of group g.
+template <int NC, int IN, int NF, int G, int S0, int QR, class Epi>
+__device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, const lds_f* in,
+                                       Epi&& epi) {
   constexpr int SP = IN / 4 + 4, NQ = IN / 16;
-  // U groups per loop trip, so every trip starts at ring slot 0
-  constexpr int U = NQ >= QRING ? 1 : QRING / NQ;
-  static_assert((U * NQ) % QRING == 0, "a loop trip starts at ring slot 0");
   const lds_f* src = in + cx.l16 * SP;
-#pragma unroll 1
-  for (int g0 = 0; g0 < groups; g0 += U) static_for<0, U>([&](auto uu) {
-    constexpr int u = decltype(uu)::value;
-    const int g = g0 + u;
+  static_for<0, G>([&](auto gg) {
+    constexpr int g = decltype(gg)::value;
     f32x4 acc[NC][QCH];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
       for (int h = 0; h < QCH; ++h) acc[c][h] = zero4();
     static_for<0, NQ>([&](auto qq) {
-      constexpr int q = decltype(qq)::value, slot = (u * NQ + q) % QRING;
+      constexpr int q = decltype(qq)::value, slot = (S0 + g * NQ + q) % QR;
       f32x4 b[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -151,7 +150,7 @@ __device__ __forceinline__ void qlayer(QRing& ring, Rsrc W, const QCx& cx, const
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[c][e % QCH] = mfma4(a[e], b[c][e], acc[c][e % QCH]);
-      qfetch<NF>(ring, W, cx.lane, slot);
+      qfetch<NF, QR>(ring, W, cx.lane, slot);
     });
     float v[NC];
 #pragma unroll
@@ -192,8 +191,8 @@ __device__ __forceinline__ void qreduce(const QCx& cx, float (&v)[NV]) {
 
 // Forward pass (NN.out, :215-259) for the 4 pairs of the tile; returns τ of the lane's pair.
 // GRAD: save σ10 for the reverse sweep.  Buffers: 0 = features / dz, 1 = A, 2 = B.
-template <int DIM, bool GRAD, int NF>
-__device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx,
+template <int DIM, bool GRAD, int NF, int QR>
+__device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx& cx,
                                               const PairIO& io, const f32x4 (&aux)[Q_NAUX],
                                               int compat) {
   const float cm = compat ? 1.f : 0.f;
@@ -221,7 +220,7 @@ __device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx
   }
   qsync();
   // ---- encoder[0] (:227); compat: the out_backgrad quirk (:435-438) stores σ10(softplus(y))
-  qlayer<2, 256, NF>(ring, W, cx, F, 2, [&](int g, const float (&v)[2]) {
+  qlayer<2, 256, NF, 2, 0 % QR, QR>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       SpSig q = sp_sig(v[c] + pick(aux[0], g));
@@ -234,7 +233,7 @@ __device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int la = 1 + 2 * blk, sa = QS_EBLK + 8 * blk;
-    qlayer<2, 128, NF>(ring, W, cx, A, 2, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 0 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         SpSig q = sp_sig(v[c] + pick(aux[la], g));
@@ -243,7 +242,7 @@ __device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx
       }
     });
     qsync();
-    qlayer<2, 128, NF>(ring, W, cx, B, 2, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -255,7 +254,7 @@ __device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx
     qsync();
   }
   // ---- encoder[-1] (:234) and the smooth max / min merge (:236-244): u = [M | m] -> B
-  qlayer<2, 128, NF>(ring, W, cx, A, 2, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 2, 0 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const float zs = v[0] + pick(aux[5], g), zg = v[1] + pick(aux[5], g);
     const float d = zs - zg;
     const float e = exp_neg10abs(d);
@@ -274,13 +273,13 @@ __device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx
   for (int i = 0; i < 3; ++i) {
     const f32x4 ba = i == 0 ? aux[6] : i == 1 ? aux[8] : aux[10];
     const f32x4 bb = i == 0 ? aux[7] : i == 1 ? aux[9] : aux[11];
-    qlayer<1, 256, NF>(ring, W, cx, B, 4, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       SpSig q = sp_sig(v[0] + pick(ba, g));
       *cx.at<256>(A, 0, g) = q.sp;
       if (GRAD) *cx.sig(QS_GBLK + 8 * i + g) = q.sg;
     });
     qsync();
-    qlayer<1, 256, NF>(ring, W, cx, A, 4, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       SpSig q = sp_sig(v[0] + pick(bb, g) + *o);
       *o = q.sp;
@@ -290,7 +289,7 @@ __device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx
   }
   // ---- generator[-2] + act (:251-252) and the head generator[-1] (:254-255)
   float part[1] = {0.f};
-  qlayer<1, 256, NF>(ring, W, cx, B, 2, [&](int g, const float (&v)[1]) {
+  qlayer<1, 256, NF, 2, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
     SpSig q = sp_sig(v[0] + pick(aux[12], g));
     part[0] = fmaf(pick(aux[13], g), q.sp, part[0]);
     if (GRAD) *cx.sig(QS_G3 + g) = q.sg;
@@ -302,8 +301,8 @@ __device__ __forceinline__ float quad_forward(QRing& ring, Rsrc W, const QCx& cx
 
 // Reverse sweep (exact, or out_backgrad when the forward stored the quirk): dτ/dxs, dτ/dxg of
 // the lane's pair, identical in all lanes of the pair.
-template <int DIM, int NF>
-__device__ __forceinline__ void quad_backward(QRing& ring, Rsrc W, const QCx& cx,
+template <int DIM, int NF, int QR>
+__device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx& cx,
                                               const PairIO& io, float tau,
                                               const f32x4 (&aux)[Q_NAUX], float (&ds)[DIM],
                                               float (&dg)[DIM]) {
@@ -314,19 +313,19 @@ __device__ __forceinline__ void quad_backward(QRing& ring, Rsrc W, const QCx& cx
   for (int g = 0; g < 2; ++g) *cx.at<128>(A, 0, g) = dd * pick(aux[13], g) * *cx.sig(QS_G3 + g);
   qsync();
   // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> B
-  qlayer<1, 128, NF>(ring, W, cx, A, 4, [&](int g, const float (&v)[1]) {
+  qlayer<1, 128, NF, 4, 16 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
     *cx.at<256>(B, 0, g) = v[0] * *cx.sig(QS_GBLK + 16 + 4 + g);
   });
   qsync();
   // ---- generator blocks, reverse (:615-618): lb: B -> A, la: A (+ B residual) -> B
 #pragma unroll 1
   for (int i = 2; i >= 0; --i) {
-    qlayer<1, 256, NF>(ring, W, cx, B, 4, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * i + g);
     });
     qsync();
     const int sb = QS_GBLK + 8 * (i - 1) + 4;   // σ10(y2) of block i - 1 (none for i = 0)
-    qlayer<1, 256, NF>(ring, W, cx, A, 4, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       const float y = v[0] + *o;
       *o = i > 0 ? y * *cx.sig(sb + g) : y;
@@ -344,7 +343,7 @@ __device__ __forceinline__ void quad_backward(QRing& ring, Rsrc W, const QCx& cx
   }
   qsync();
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1): F -> A
-  qlayer<2, 128, NF>(ring, W, cx, F, 2, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 2, 16 % QR, QR>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) *cx.at<128>(A, c, g) = v[c] * *cx.sig(QS_EBLK + 12 + 2 * g + c);
   });
@@ -354,12 +353,12 @@ __device__ __forceinline__ void quad_backward(QRing& ring, Rsrc W, const QCx& cx
 #pragma unroll
   for (int blk = 1; blk >= 0; --blk) {
     const int sa = QS_EBLK + 8 * blk, sbelow = blk ? QS_EBLK + 4 : QS_E0;
-    qlayer<2, 128, NF>(ring, W, cx, A, 2, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 0 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) *cx.at<128>(B, c, g) = v[c] * *cx.sig(sa + 2 * g + c);
     });
     qsync();
-    qlayer<2, 128, NF>(ring, W, cx, B, 2, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -373,7 +372,7 @@ __device__ __forceinline__ void quad_backward(QRing& ring, Rsrc W, const QCx& cx
   float acc[2 * DIM];
 #pragma unroll
   for (int i = 0; i < 2 * DIM; ++i) acc[i] = 0.f;
-  qlayer<2, 128, NF>(ring, W, cx, A, 4, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 4, 0 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const int f = cx.w * 64 + 16 * g + 4 * cx.og + cx.kb;
     const int fb = f & 127;
     float bw[DIM];
@@ -416,6 +415,7 @@ template <int DIM, int KIND>
 __global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
   constexpr bool GRAD = KIND != K_TAU && KIND != K_TRAVEL;
   constexpr int NF = GRAD ? Q_NF_ALL : Q_NF_FWD;
+  constexpr int QR = GRAD ? QRING : QRING_TAU;
   __shared__ float smem[Q_LDS_FLOATS];
   const QCx cx = quad_cx((lds_f*)smem);
   const Rsrc W = make_rsrc(a.P + OFF_QUAD + cx.w * Q_STREAM, Q_STREAM * 4);
@@ -424,18 +424,18 @@ __global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
 #pragma unroll
   for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
   aux[13][2] = a.P[OFF_BIAS + B_G4B];
-  QRing ring;
+  QRing<QR> ring;
   ring.next = 0;
 #pragma unroll
-  for (int s = 0; s < QRING; ++s) qfetch<NF>(ring, W, cx.lane, s);
+  for (int s = 0; s < QR; ++s) qfetch<NF, QR>(ring, W, cx.lane, s);
   const int64_t ntiles = (a.n + QPAIRS - 1) / QPAIRS;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t pair = tile * QPAIRS + (cx.lane & 3);
     PairIO io;
     const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
-    const float tau = quad_forward<DIM, GRAD, NF>(ring, W, cx, io, aux, a.compat);
+    const float tau = quad_forward<DIM, GRAD, NF, QR>(ring, W, cx, io, aux, a.compat);
     float ds[DIM], dg[DIM];
-    if constexpr (GRAD) quad_backward<DIM, NF>(ring, W, cx, io, tau, aux, ds, dg);
+    if constexpr (GRAD) quad_backward<DIM, NF, QR>(ring, W, cx, io, tau, aux, ds, dg);
     const bool store = cx.w == 0 && cx.lane < QPAIRS && pair < a.n;
     store_field<DIM, KIND>(a, pair, ok, store, tau, io, ds, dg);
   }
@@ -453,10 +453,10 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
 #pragma unroll
   for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
   aux[13][2] = a.P[OFF_BIAS + B_G4B];
-  QRing ring;
+  QRing<QRING> ring;
   ring.next = 0;
 #pragma unroll
-  for (int s = 0; s < QRING; ++s) qfetch<Q_NF_ALL>(ring, W, cx.lane, s);
+  for (int s = 0; s < QRING; ++s) qfetch<Q_NF_ALL, QRING>(ring, W, cx.lane, s);
   const int cap = a.max_iter + 1;
   const int64_t rows = (int64_t)cap + 1;
   const int64_t ntiles = (a.q + QPAIRS - 1) / QPAIRS;
@@ -486,9 +486,9 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
     int it = 0;
     for (; it < cap; ++it) {
       if (!__any(active)) break;
-      const float tau = quad_forward<DIM, true, Q_NF_ALL>(ring, W, cx, io, aux, a.compat);
+      const float tau = quad_forward<DIM, true, Q_NF_ALL, QRING>(ring, W, cx, io, aux, a.compat);
       float ds[DIM], dg[DIM], vs[DIM], vg[DIM];
-      quad_backward<DIM, Q_NF_ALL>(ring, W, cx, io, tau, aux, ds, dg);
+      quad_backward<DIM, Q_NF_ALL, QRING>(ring, W, cx, io, tau, aux, ds, dg);
       path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
       if (active) {
 #pragma unroll

@@ -212,6 +212,18 @@ int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const f
                       float* diff, float* gv, float* gw4, float* gb4, float* partial,
                       hipStream_t stream);
 
+/* fp32 GEMM of the training step on hand-written MFMA kernels (pntf_gemm.hip; the Linear
+ * layers of the Taylor tape: forward X·Wᵀ, input gradient gY·W, weight gradient gYᵀ·X):
+ * C (M x N, row stride ldc) = beta*C + A·B with A(m,k) = ta ? A[k*lda + m] : A[m*lda + k] and
+ * B(k,n) = tb ? B[n*ldb + k] : B[k*ldb + n].  N must be a multiple of 128.  Long K is split
+ * over workgroups (deterministic partial sums in `work`, pntf_tt_gemm_work_floats(M, N, K)
+ * floats; may be NULL when that is 0).  beta == 0 never reads C. */
+size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K);
+int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                 const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
+                 size_t work_floats, hipStream_t stream);
+const char* pntf_tt_gemm_last_error(void);
+
 /* torch.optim.AdamW update of one parameter tensor (the reference's optimizer, :959-961):
  * p, grad, exp_avg, exp_avg_sq (n); `step` = the step count after this update (>= 1). */
 int pntf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,

@@ -1,0 +1,313 @@
+// fp32 GEMMs of the training step (pntf/train.py) on v_mfma_f32_32x32x2_f32, replacing the
+// library GEMMs the Taylor tape used: per Linear of NN.out_laplace (model_res_sigmoid_multi.py
+// :710-848, differentiated by loss.backward() at :1048)
+//   forward          Y (rows x N)  = X (rows x K) · Wᵀ          (A row-major, B = Wᵀ)
+//   input gradient   gX (rows x K) (+)= gY (rows x N) · W       (A row-major, B row-major)
+//   weight gradient  gW (N x K)    = gYᵀ · X  over all rows     (A = gYᵀ, B row-major, split-K)
+// C = beta·C + A·B with A(m, k) = TA ? A[k·lda + m] : A[m·lda + k] and
+// B(k, n) = TB ? B[n·ldb + k] : B[k·ldb + n].
+//
+// Workgroup tile 128 x 128, K chunks of 16 staged through LDS (double-buffered, one barrier per
+// chunk, the next chunk's global loads in flight during the current chunk's MFMAs); 4 waves,
+// each a 64 x 64 block = 2 x 2 MFMA tiles of 32 x 32 (64 accumulators).  Per chunk and wave:
+// 32 MFMAs of 64 cycles against 4 ds_read_b32 per k-step and 2 float4 global loads per lane,
+// so the loop is MFMA-bound.  N must be a multiple of 128 (the layer widths 128 / 256); M and
+// K are arbitrary (zero-filled / predicated edges).  Split-K (blockIdx.z) writes partial tiles
+// to `work` and a second kernel sums them in split order: deterministic, no atomics.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include "pntf.h"
+
+namespace pntf_gemm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#ifndef PNTF_GEMM_BK
+#define PNTF_GEMM_BK 16
+#endif
+#ifndef PNTF_GEMM_SPLITS
+#define PNTF_GEMM_SPLITS 512
+#endif
+#ifndef PNTF_GEMM_BM
+#define PNTF_GEMM_BM 128
+#endif
+constexpr int BM = PNTF_GEMM_BM, BN = 128, BK = PNTF_GEMM_BK;
+constexpr int RB = BM / 64;          // 32-row MFMA blocks per wave (waves are 2 x 2)
+constexpr int GLA = BM * BK / 1024;  // float4 global loads per lane per chunk: A
+constexpr int GLB = BN * BK / 1024;  //                                        B
+constexpr int LSA = BM + 32;         // LDS row strides (≡ 32 mod 64: conflict-free halves)
+constexpr int LS = 160;   // LDS row stride (floats): lanes 32-63 read the next k row in the
+                          // other 32 banks (stride ≡ 32 mod 64), conflict-free
+
+struct GemmArgs {
+  const float* A;
+  const float* B;
+  float* C;
+  float* work;
+  int64_t M, N, K, lda, ldb, ldc, kper;
+  float beta;
+};
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
+  __shared__ float As[2][BK * LSA];
+  __shared__ float Bs[2][BK * LS];
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w & 1, wn = w >> 1;
+  const int64_t m0 = (int64_t)blockIdx.y * BM;
+  const int64_t n0 = (int64_t)blockIdx.x * BN;
+  const int64_t kb = (int64_t)blockIdx.z * g.kper;
+  const int64_t ke = kb + g.kper < g.K ? kb + g.kper : g.K;
+  const int nchunks = (int)((ke - kb + BK - 1) / BK);
+
+  // global -> registers: 2 float4 per lane for A and for B
+  f32x4 ra[GLA], rb[GLB];
+  auto gload = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < GLA; ++i) {
+      const int idx = t + 256 * i;
+      if (TA) {   // rows k (BK) x m (BM) contiguous: float4 along m
+        const int k = idx / (BM / 4), m = 4 * (idx % (BM / 4));
+        const int64_t gk = k0 + k, gm = m0 + m;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (gk < ke) {
+          if (gm + 3 < g.M) {
+            v = *reinterpret_cast<const f32x4*>(g.A + gk * g.lda + gm);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gm + e < g.M ? g.A[gk * g.lda + gm + e] : 0.f;
+          }
+        }
+        ra[i] = v;
+      } else {    // rows m (BM) x k (BK) contiguous: float4 along k
+        const int m = idx / (BK / 4), k = 4 * (idx % (BK / 4));
+        const int64_t gk = k0 + k, gm = m0 + m;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (gm < g.M) {
+          if (gk + 3 < ke) {
+            v = *reinterpret_cast<const f32x4*>(g.A + gm * g.lda + gk);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gk + e < ke ? g.A[gm * g.lda + gk + e] : 0.f;
+          }
+        }
+        ra[i] = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GLB; ++i) {
+      const int idx = t + 256 * i;
+      if (TB) {   // B(k, n) = B[n·ldb + k]: float4 along k
+        const int n = idx / (BK / 4), k = 4 * (idx % (BK / 4));
+        const int64_t gk = k0 + k, gn = n0 + n;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (gk + 3 < ke) {
+          v = *reinterpret_cast<const f32x4*>(g.B + gn * g.ldb + gk);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gk + e < ke ? g.B[gn * g.ldb + gk + e] : 0.f;
+        }
+        rb[i] = v;
+      } else {    // B(k, n) = B[k·ldb + n]: float4 along n
+        const int k = idx >> 5, n = 4 * (idx & 31);
+        const int64_t gk = k0 + k;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (gk < ke) v = *reinterpret_cast<const f32x4*>(g.B + gk * g.ldb + n0 + n);
+        rb[i] = v;
+      }
+    }
+  };
+  // registers -> LDS image [k][m] / [k][n]
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < GLA; ++i) {
+      const int idx = t + 256 * i;
+      if (TA) {
+        const int k = idx / (BM / 4), m = 4 * (idx % (BM / 4));
+        *reinterpret_cast<f32x4*>(&As[buf][k * LSA + m]) = ra[i];
+      } else {
+        const int m = idx / (BK / 4), k = 4 * (idx % (BK / 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) As[buf][(k + e) * LSA + m] = ra[i][e];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GLB; ++i) {
+      const int idx = t + 256 * i;
+      if (TB) {
+        const int n = idx / (BK / 4), k = 4 * (idx % (BK / 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Bs[buf][(k + e) * LS + n] = rb[i][e];
+      } else {
+        const int k = idx >> 5, n = 4 * (idx & 31);
+        *reinterpret_cast<f32x4*>(&Bs[buf][k * LS + n]) = rb[i];
+      }
+    }
+  };
+
+  f32x16 acc[RB][2];
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nchunks > 0) {
+    gload(kb);
+    lstore(0);
+  }
+  __syncthreads();
+  const int am = wm * (BM / 2) + (lane & 31), bn = wn * 64 + (lane & 31), kh = lane >> 5;
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) gload(kb + (int64_t)(c + 1) * BK);
+    const float* as = As[buf];
+    const float* bs = Bs[buf];
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int kr = 2 * kk + kh;
+      float a[RB];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) a[i] = as[kr * LSA + am + 32 * i];
+      const float b0 = bs[kr * LS + bn], b1 = bs[kr * LS + bn + 32];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b0, acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b1, acc[i][1], 0, 0, 0);
+      }
+    }
+    if (more) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // D row of register r in lane half h: (r & 3) + 8·(r >> 2) + 4·h, column lane & 31
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (BM / 2) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+        if (row < g.M) {
+          if (split) {
+            g.work[((int64_t)blockIdx.z * g.M + row) * g.N + col] = acc[i][j][r];
+          } else {
+            float* cp = g.C + row * g.ldc + col;
+            *cp = g.beta != 0.f ? fmaf(g.beta, *cp, acc[i][j][r]) : acc[i][j][r];
+          }
+        }
+      }
+}
+
+// Split-K reduction, two passes, fixed order (deterministic):
+//   pass 1: group zg (blockIdx.y) sums splits [RG·zg, RG·zg + RG) into work[RG·zg] (in place;
+//           that slot is read first by the same thread), 4 independent loads in flight;
+//   pass 2: C = beta·C + Σ_zg work[RG·zg].
+constexpr int RG = 32;
+__global__ void gemm_reduce1_kernel(float* __restrict__ work, int splits, int64_t MN) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= MN) return;
+  const int z0 = blockIdx.y * RG, z1 = z0 + RG < splits ? z0 + RG : splits;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  int z = z0;
+  for (; z + 4 <= z1; z += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s[u] += work[(int64_t)(z + u) * MN + o];
+  for (; z < z1; ++z) s[0] += work[(int64_t)z * MN + o];
+  work[(int64_t)z0 * MN + o] = (s[0] + s[1]) + (s[2] + s[3]);
+}
+__global__ void gemm_reduce2_kernel(const float* __restrict__ work, int splits, int64_t M,
+                                    int64_t N, float* __restrict__ C, int64_t ldc, float beta) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= M * N) return;
+  const int64_t row = o / N, col = o % N;
+  float s = 0.f;
+  for (int z = 0; z < splits; z += RG) s += work[(int64_t)z * M * N + o];
+  float* cp = C + row * ldc + col;
+  *cp = beta != 0.f ? fmaf(beta, *cp, s) : s;
+}
+
+thread_local char g_err[512] = "";
+
+int num_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return 256;
+  return cus;
+}
+
+// Split-K factor: enough workgroups for 2 per CU, chunks of at least 1024 rows of K.
+int64_t splits_for(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + BM - 1) / BM) * (N / BN);
+  int64_t s = (2 * (int64_t)num_cus() + tiles - 1) / tiles;
+  const int64_t kmax = (K + 1023) / 1024;
+  if (s > kmax) s = kmax;
+  if (s > PNTF_GEMM_SPLITS) s = PNTF_GEMM_SPLITS;
+  return s < 1 ? 1 : s;
+}
+
+}  // namespace pntf_gemm
+
+using namespace pntf_gemm;
+
+extern "C" {
+
+size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int64_t s = splits_for(M, N, K);
+  return s > 1 ? (size_t)(s * M * N) : 0;
+}
+
+int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                 const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
+                 size_t work_floats, hipStream_t stream) {
+  if (M < 0 || N < 0 || K < 0 || N % BN != 0) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: need M, K >= 0 and N a multiple of %d", BN);
+    return PNTF_ERR_ARG;
+  }
+  if (M == 0 || N == 0) return PNTF_OK;
+  if (!A || !B || !C) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: null pointer");
+    return PNTF_ERR_ARG;
+  }
+  const int64_t s = K > 0 ? splits_for(M, N, K) : 1;
+  if (s > 1 && (!work || work_floats < (size_t)(s * M * N))) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: work buffer too small");
+    return PNTF_ERR_WORKSPACE;
+  }
+  GemmArgs g{A, B, C, work, M, N, K, lda, ldb, ldc, 0, beta};
+  g.kper = ((K + s - 1) / s + BK - 1) / BK * BK;
+  if (g.kper < BK) g.kper = BK;
+  dim3 grid((unsigned)(N / BN), (unsigned)((M + BM - 1) / BM), (unsigned)s), block(256);
+  if (ta && tb) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, stream, g);
+  else if (ta) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, block, 0, stream, g);
+  else if (tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, block, 0, stream, g);
+  else hipLaunchKernelGGL((gemm_kernel<false, false>), grid, block, 0, stream, g);
+  if (s > 1) {
+    const int64_t n = M * N;
+    const unsigned nb = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(gemm_reduce1_kernel, dim3(nb, (unsigned)((s + RG - 1) / RG)), dim3(256),
+                       0, stream, work, (int)s, n);
+    hipLaunchKernelGGL(gemm_reduce2_kernel, dim3(nb), dim3(256), 0, stream, work, (int)s, M, N,
+                       C, ldc, beta);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: %s", hipGetErrorString(e));
+    return PNTF_ERR_HIP;
+  }
+  return PNTF_OK;
+}
+
+const char* pntf_tt_gemm_last_error(void) { return g_err; }
+
+}  // extern "C"

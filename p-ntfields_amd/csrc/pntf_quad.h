@@ -44,10 +44,11 @@ constexpr int Q_NF_ALL = 2 * Q_NF_FWD;
 constexpr int QBUF = 2 * 16 * 68;           // activation buffer: 2 columns x 16 lane rows x 68
 constexpr int QNSIG = 48;                   // saved σ10 slots per wave (64 floats each)
 constexpr int Q_RED = 3 * QBUF + Q_WAVES * QNSIG * 64;
-// 21504 floats = 84 KiB: more than half the CU's LDS, so one workgroup per CU (the second
+constexpr int Q_BW = Q_RED + Q_WAVES * 12 * 4;   // 2π·B of the tile's 4 pairs: [pair][dim][128]
+// 24576 floats = 96 KiB: more than half the CU's LDS, so one workgroup per CU (the second
 // wave per SIMD corrupts MFMA results here)
-constexpr int Q_LDS_FLOATS = 21504;
-static_assert(Q_RED + Q_WAVES * 12 * 4 <= Q_LDS_FLOATS, "quad LDS budget");
+constexpr int Q_LDS_FLOATS = 24576;
+static_assert(Q_BW + QPAIRS * 6 * H <= Q_LDS_FLOATS, "quad LDS budget");
 // σ slots (forward order): encoder[0] 0-3, encoder blocks a0 4-7, b0 8-11, a1 12-15,
 // b1 16-19 (group·2 + column), merge switch 20-21, generator a_i 22 + 8i + g, b_i 26 + 8i + g,
 // generator[-2] 46-47.
@@ -96,6 +97,8 @@ struct QCx {
   __device__ lds_f* buf(int b) const { return lds + b * QBUF; }
   __device__ lds_f* sig(int slot) const { return lds + 3 * QBUF + (w * QNSIG + slot) * 64 + lane; }
   __device__ lds_f* red(int wave, int v) const { return lds + Q_RED + (wave * 12 + v) * 4; }
+  // 2π·B[d][f] of pair j of the tile (staged once per tile by quad_stage_b)
+  __device__ lds_f* bw(int j, int d) const { return lds + Q_BW + (j * 6 + d) * H; }
   // compact (row, pair) slot of a layer with OUT rows, group g, column c in a buffer read by
   // the next layer (its in features = OUT: row stride OUT/4 + 4)
   template <int OUT>
@@ -210,7 +213,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
       const int f = fb + 32 * m;
       float q = 0.f;
 #pragma unroll
-      for (int d = 0; d < DIM; ++d) q = fmaf(xc[d], TWO_PI * io.Bw[d * H + f], q);
+      for (int d = 0; d < DIM; ++d) q = fmaf(xc[d], cx.bw(j, d)[f], q);
       float sn, cs;
       sincos_fast(q, sn, cs);
       lds_f* p = F + (c * 16 + 4 * (f & 3) + j) * 68 + (f >> 2);
@@ -377,7 +380,7 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
     const int fb = f & 127;
     float bw[DIM];
 #pragma unroll
-    for (int d = 0; d < DIM; ++d) bw[d] = TWO_PI * io.Bw[d * H + fb];
+    for (int d = 0; d < DIM; ++d) bw[d] = cx.bw(cx.lane & 3, d)[fb];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       float q = 0.f;
@@ -396,6 +399,20 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
     ds[d] = acc[d];
     dg[d] = acc[DIM + d];
   }
+}
+
+// The tile's Fourier matrices (2π·B of each pair's env) into LDS, once per tile: the per-step
+// feature and fold reads then never wait on vmcnt, which would drain the weight ring.  The
+// caller's next barrier (the one after the features) orders the writes before any read; the
+// previous tile's last reads (its fold) precede the qreduce barrier.
+template <int DIM>
+__device__ __forceinline__ void quad_stage_b(const QCx& cx, const PairIO& io) {
+  // thread (w, lane): pair j = lane & 3 (its own io), rows d, features (lane >> 2) + 16 i
+  const int j = cx.lane & 3, f0 = (cx.lane >> 2) + 16 * cx.w;
+#pragma unroll
+  for (int d = 0; d < DIM; ++d)
+#pragma unroll
+    for (int i = 0; i < H / 64; ++i) cx.bw(j, d)[f0 + 64 * i] = TWO_PI * io.Bw[d * H + f0 + 64 * i];
 }
 
 __device__ __forceinline__ QCx quad_cx(lds_f* lds) {
@@ -433,6 +450,8 @@ __global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
     const int64_t pair = tile * QPAIRS + (cx.lane & 3);
     PairIO io;
     const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
+    quad_stage_b<DIM>(cx, io);
+    qsync();
     const float tau = quad_forward<DIM, GRAD, NF, QR>(ring, W, cx, io, aux, a.compat);
     float ds[DIM], dg[DIM];
     if constexpr (GRAD) quad_backward<DIM, NF, QR>(ring, W, cx, io, tau, aux, ds, dg);
@@ -464,6 +483,8 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
     const int64_t qi = tile * QPAIRS + (cx.lane & 3);
     PairIO io;
     const bool ok = load_pair<DIM>(a.xp0, a.Btab, a.env, a.q, a.n_env, qi, io);
+    quad_stage_b<DIM>(cx, io);
+    qsync();
     const bool store = cx.w == 0 && cx.lane < QPAIRS && qi < a.q;
     float* prow = a.path + (store ? qi : 0) * rows * 2 * DIM;
     auto dist = [&]() {

@@ -93,7 +93,8 @@ UNITS = (
     + [("residual_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_RESIDUAL"])
        for d in (3, 6)]
     + [("util", "pntf_kernels.hip", ["-DPNTF_UTIL"]), ("capi", "pntf_capi.hip", []),
-       ("train", "pntf_train.hip", []), ("mesh", "pntf_mesh.hip", [])]
+       ("train", "pntf_train.hip", []), ("gemm", "pntf_gemm.hip", []),
+       ("mesh", "pntf_mesh.hip", [])]
 )
 
 

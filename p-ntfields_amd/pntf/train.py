@@ -8,7 +8,7 @@ with `torch.optim.AdamW(lr=1e-3, weight_decay=0.1)` (:959-961) — models/model_
 Taylor-mode graph `NN.out_laplace` (:710-848) with autograd; here the adjoint is explicit:
 
   forward  Φ planes (tt_fourier) → per Linear: one fp32 GEMM over all R·M Taylor rows
-           (torch.mm → hipBLASLt) + a fused bias/residual/act_laplace kernel (tt_act_fwd) that
+           (pntf_tt_gemm, csrc/pntf_gemm.hip) + a fused bias/residual/act_laplace kernel (tt_act_fwd) that
            keeps the pre-activation as the tape → merge (tt_merge_fwd) → generator → generator[3]
   head     generator[4] + actout_laplace + Model.Loss forward and backward in one kernel
            (tt_head_loss): diff per pair and d(Σdiff)/d(generator[3] output)
@@ -19,8 +19,9 @@ Taylor-mode graph `NN.out_laplace` (:710-848) with autograd; here the adjoint is
 
 Layout: a Taylor tensor of M points and width W is (R, M, W) fp32, R = 1 + 2·ndir planes
 [value | ∂ (ndir) | diagonal ∂² (ndir)], ndir = dim in the encoder and 2·dim after the merge.
-The GEMMs are plain library GEMMs (fp32, TF32 off); every elementwise stage is a HIP kernel
-of libpntf.so (csrc/pntf_train.hip).  There is no CPU path.
+The GEMMs are the library's own fp32 MFMA kernels (pntf_tt_gemm: v_mfma_f32_32x32x2_f32,
+128 x 128 LDS tiles, deterministic split-K for the weight gradients); every elementwise stage
+is a HIP kernel of libpntf.so (csrc/pntf_train.hip).  There is no CPU path and no vendor GEMM.
 """
 import ctypes
 
@@ -64,6 +65,40 @@ def _partial(device):
     return buf
 
 
+_work_cache = {}
+
+
+def _work(device, floats):
+    """Split-K partial sums of pntf_tt_gemm per (device, stream), grown on demand."""
+    stream = torch.cuda.current_stream(device)
+    key = (device.index, stream.cuda_stream)
+    buf = _work_cache.get(key)
+    if buf is None or buf.numel() < floats:
+        buf = torch.empty(max(int(floats), 1), dtype=torch.float32, device=device)
+        buf.record_stream(stream)
+        _work_cache[key] = buf
+    return buf
+
+
+def gemm(C, A, B, ta, tb, beta=0.0):
+    """C (M, N) = beta·C + op(A) · op(B) on the library's MFMA GEMM (pntf_tt_gemm):
+    op(A) = A (M, K) or, ta, A (K, M) transposed; op(B) = B (K, N) or, tb, B (N, K)
+    transposed.  All fp32 contiguous 2-D device tensors."""
+    lib = _lib.load()
+    M, N = C.shape
+    K = A.shape[0] if ta else A.shape[1]
+    if (B.shape[1] if tb else B.shape[0]) != K or (A.shape[1] if ta else A.shape[0]) != M or \
+            (B.shape[0] if tb else B.shape[1]) != N:
+        raise PntfError("gemm shape mismatch")
+    nw = int(lib.pntf_tt_gemm_work_floats(M, N, K))
+    work = _work(C.device, nw) if nw else None
+    st = lib.pntf_tt_gemm(int(ta), int(tb), M, N, K, _vp(A), A.shape[1], _vp(B), B.shape[1],
+                          _vp(C), C.shape[1], float(beta), _vp(work), nw,
+                          _stream(C.device))
+    if st != 0:
+        raise PntfError("pntf_tt_gemm: " + lib.pntf_tt_gemm_last_error().decode())
+
+
 class _Tape:
     """Forward tape of one loss evaluation: (name, input planes, pre-activation planes, act,
     has_residual) per Linear, in execution order."""
@@ -81,7 +116,7 @@ class _Tape:
         R, M, K = x3.shape
         N = W.shape[0]
         y = torch.empty((R, M, N), dtype=torch.float32, device=self.dev)
-        torch.mm(x3.view(R * M, K), W.t(), out=y.view(R * M, N))
+        gemm(y.view(R * M, N), x3.view(R * M, K), W, ta=False, tb=True)
         h = torch.empty_like(y) if act else None
         check(self.lib.pntf_tt_act_fwd((R - 1) // 2, _vp(y), _vp(h), _vp(b), _vp(res), M, N,
                                        int(act), self.s), "pntf_tt_act_fwd")
@@ -89,27 +124,11 @@ class _Tape:
         return h if act else y
 
 
-_SPLIT_ROWS = 8192      # rows per split-K chunk of a weight-gradient GEMM
-_SPLIT_MAX = 64
-
-
 def weight_grad(g2, x2, out):
     """out (N, K) = g2ᵀ (N, rows) · x2 (rows, K).  The reduction runs over every Taylor row of
-    every point (rows = R·M, 10⁵-10⁶) into a tiny 128/256-square output: as one GEMM it has
-    only a handful of output tiles for 256 CUs (measured 15-42 TFLOP/s).  Split-K instead: S
-    row chunks as one batched GEMM (S·tiles workgroups), then a sum over the S partials."""
-    rows, N = g2.shape
-    K = x2.shape[1]
-    S = min(_SPLIT_MAX, rows // _SPLIT_ROWS)
-    if S < 2:
-        torch.mm(g2.t(), x2, out=out)
-        return
-    c = rows // S
-    main = c * S
-    part = torch.bmm(g2[:main].view(S, c, N).transpose(1, 2), x2[:main].view(S, c, K))
-    torch.sum(part, dim=0, out=out)
-    if main < rows:
-        torch.addmm(out, g2[main:].t(), x2[main:], out=out)
+    every point (rows = R·M, 10⁵-10⁶) into a tiny 128/256-square output, so pntf_tt_gemm
+    splits the rows over ~2 workgroups per CU and sums the partials in a fixed order."""
+    gemm(out, g2, x2, ta=True, tb=False)
 
 
 def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
@@ -125,8 +144,6 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
         for g in grads.values():
             g.zero_()
         return torch.empty(0, dtype=torch.float32, device=dev)
-    if torch.backends.cuda.matmul.allow_tf32:
-        raise PntfError("TF32 GEMMs are enabled; the training step computes in fp32")
     tape = _Tape(params, dim, dev)
     s = tape.s
     Re, Rg = 1 + 2 * dim, 1 + 4 * dim
@@ -171,10 +188,10 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
             # the block input also fed the residual add: accumulate into that branch's
             # gradient in place (beta = 1, no copy); it is not read again
             gx = pending.pop()
-            torch.addmm(gx.view(R * M, K), g2, W, out=gx.view(R * M, K))
+            gemm(gx.view(R * M, K), g2, W, ta=False, tb=False, beta=1.0)
         else:
             gx = torch.empty((R, M, K), dtype=torch.float32, device=dev)
-            torch.mm(g2, W, out=gx.view(R * M, K))
+            gemm(gx.view(R * M, K), g2, W, ta=False, tb=False)
         g = gx
         if name == "generator.0":
             gz = torch.empty((Re, 2 * n, H), dtype=torch.float32, device=dev)

@@ -353,3 +353,53 @@ def test_arm_model_train_two_epochs(tmp_path):
         assert torch.equal(a.cpu(), b.cpu()), k
     xp = torch.from_numpy(synth.make_box_pairs(64, 6, seed=94)).cuda()
     assert torch.equal(model.Gradient(xp), m2.Gradient(xp))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ta,tb,M,N,K,beta", [
+    (False, True, 40001, 256, 256, 0.0),    # forward X·Wᵀ (generator)
+    (False, True, 129, 128, 256, 0.0),      # forward, encoder[0], ragged rows
+    (False, False, 70007, 128, 256, 1.0),   # input gradient gY·W + residual branch
+    (False, False, 1, 256, 128, 0.0),
+    (True, False, 256, 256, 260013, 0.0),   # weight gradient gYᵀ·X (split-K)
+    (True, False, 128, 256, 1000, 0.0),     # weight gradient, short reduction
+    (True, True, 128, 128, 77, 0.5),
+])
+def test_mfma_gemm_vs_fp64(ta, tb, M, N, K, beta):
+    """pntf_tt_gemm (csrc/pntf_gemm.hip) against an fp64 matmul of the same fp32 operands, for
+    the three layouts of the training step, ragged M / K edges and split-K.  Bound: fp32
+    accumulation over K terms, |err| <= 1e-5·sqrt(K)·(|A|·|B|) elementwise."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    ref = (A.double().t() if ta else A.double()) @ (B.double().t() if tb else B.double())
+    ref = ref + beta * C0.double()
+    C = C0.to(dev)
+    train.gemm(C, A.to(dev), B.to(dev), ta, tb, beta)
+    scale = (A.double().abs().t() if ta else A.double().abs()) @ \
+        (B.double().abs().t() if tb else B.double().abs())
+    err = (C.cpu().double() - ref).abs()
+    assert torch.all(err <= 1e-5 * np.sqrt(K) * scale + 1e-6), float((err / scale).max())
+
+
+@pytest.mark.gpu
+def test_training_uses_no_vendor_gemm():
+    """The training step's GEMMs are the library's own MFMA kernels: a profiled
+    Loss + backward launches gemm_kernel and no Tensile (Cijk_*) / hipBLASLt kernel."""
+    from torch.profiler import ProfilerActivity, profile
+    dev = torch.device("cuda:0")
+    f = load("train_d3.npz")
+    model, net = _nets(3, weights(), dev)
+    loss, _, _ = _loss(model, f, 3, dev)
+    loss.backward()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        loss, _, _ = _loss(model, f, 3, dev)
+        loss.backward()
+        torch.cuda.synchronize()
+    names = [e.key for e in prof.key_averages()]
+    assert any("gemm_kernel" in n for n in names), names
+    assert not any("Cijk" in n or "hipblaslt" in n.lower() for n in names), names

@@ -66,6 +66,35 @@ def split_probe(pairs=20000):
     print(json.dumps(out, indent=1))
 
 
+def mfma_probe(pairs=20000):
+    """The library's own MFMA GEMM (pntf.train.gemm, csrc/pntf_gemm.hip) on the same shapes,
+    TFLOP/s, beside the torch (hipBLASLt) GEMM of the same layout."""
+    sys.path.insert(0, __file__.rsplit("/tools/", 1)[0] + "/p-ntfields_amd")
+    from pntf.train import gemm
+    dev = torch.device("cuda:0")
+    out = {}
+    for tag, rows, K, N in (("gen", 13 * pairs, 256, 256), ("enc", 7 * 2 * pairs, 128, 128),
+                            ("enc0", 7 * 2 * pairs, 256, 128), ("g3", 13 * pairs, 256, 128)):
+        X = torch.randn(rows, K, device=dev)
+        G = torch.randn(rows, N, device=dev)
+        W = torch.randn(N, K, device=dev)
+        Y = torch.empty(rows, N, device=dev)
+        GX = torch.empty(rows, K, device=dev)
+        GW = torch.empty(N, K, device=dev)
+        fl = 2.0 * rows * K * N / 1e9
+        r = {"fwd": fl / timeit(lambda: gemm(Y, X, W, False, True)),
+             "fwd_torch": fl / timeit(lambda: torch.mm(X, W.t(), out=Y)),
+             "bwdx": fl / timeit(lambda: gemm(GX, G, W, False, False)),
+             "bwdx_torch": fl / timeit(lambda: torch.mm(G, W, out=GX)),
+             "bwdw": fl / timeit(lambda: gemm(GW, G, X, True, False)),
+             "bwdw_torch": fl / timeit(lambda: torch.mm(G.t(), X, out=GW))}
+        out[tag] = {k: round(v, 1) for k, v in r.items()}
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
-    main()
-    split_probe(int(sys.argv[1]) if len(sys.argv) > 1 else 20000)
+    if len(sys.argv) > 2 and sys.argv[2] == "mfma":
+        mfma_probe(int(sys.argv[1]))
+    else:
+        main()
+        split_probe(int(sys.argv[1]) if len(sys.argv) > 1 else 20000)

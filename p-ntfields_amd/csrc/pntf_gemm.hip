@@ -7,11 +7,13 @@
 // C = beta·C + A·B with A(m, k) = TA ? A[k·lda + m] : A[m·lda + k] and
 // B(k, n) = TB ? B[n·ldb + k] : B[k·ldb + n].
 //
-// Workgroup tile 128 x 128, K chunks of 16 staged through LDS (double-buffered, one barrier per
+// Workgroup tile 128 x 128, K chunks of 8 staged through LDS (double-buffered, one barrier per
 // chunk, the next chunk's global loads in flight during the current chunk's MFMAs); 4 waves,
 // each a 64 x 64 block = 2 x 2 MFMA tiles of 32 x 32 (64 accumulators).  Per chunk and wave:
-// 32 MFMAs of 64 cycles against 4 ds_read_b32 per k-step and 2 float4 global loads per lane,
-// so the loop is MFMA-bound.  N must be a multiple of 128 (the layer widths 128 / 256); M and
+// 16 MFMAs of 64 cycles; the chunk's LDS operands are read before its MFMAs (one latency per
+// chunk), and interior chunks load without predication (a wave-uniform test).  Small LDS
+// (20 KiB) lets 3 workgroups share a CU, so one's barrier hides behind the others' MFMAs
+// (tools/gemm_probe.py, tests/diag/gemm_variants.py: chunks of 8 beat 16 and 32).  N must be a multiple of 128 (the layer widths 128 / 256); M and
 // K are arbitrary (zero-filled / predicated edges).  Split-K (blockIdx.z) writes partial tiles
 // to `work` and a second kernel sums them in split order: deterministic, no atomics.
 #include <hip/hip_runtime.h>
@@ -25,7 +27,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #ifndef PNTF_GEMM_BK
-#define PNTF_GEMM_BK 16
+#define PNTF_GEMM_BK 8
 #endif
 #ifndef PNTF_GEMM_SPLITS
 #define PNTF_GEMM_SPLITS 512
@@ -65,7 +67,32 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
 
   // global -> registers: 2 float4 per lane for A and for B
   f32x4 ra[GLA], rb[GLB];
-  auto gload = [&](int64_t k0) {
+  // interior chunks (the whole tile in range: a wave-uniform test) load without predication
+  auto gload_fast = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < GLA; ++i) {
+      const int idx = t + 256 * i;
+      if (TA) {
+        const int k = idx / (BM / 4), m = 4 * (idx % (BM / 4));
+        ra[i] = *reinterpret_cast<const f32x4*>(g.A + (k0 + k) * g.lda + m0 + m);
+      } else {
+        const int m = idx % BM, k = 4 * (idx / BM);
+        ra[i] = *reinterpret_cast<const f32x4*>(g.A + (m0 + m) * g.lda + k0 + k);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GLB; ++i) {
+      const int idx = t + 256 * i;
+      if (TB) {
+        const int n = idx % BN, k = 4 * (idx / BN);
+        rb[i] = *reinterpret_cast<const f32x4*>(g.B + (n0 + n) * g.ldb + k0 + k);
+      } else {
+        const int k = idx >> 5, n = 4 * (idx & 31);
+        rb[i] = *reinterpret_cast<const f32x4*>(g.B + (k0 + k) * g.ldb + n0 + n);
+      }
+    }
+  };
+  auto gload_edge = [&](int64_t k0) {
 #pragma unroll
     for (int i = 0; i < GLA; ++i) {
       const int idx = t + 256 * i;
@@ -82,8 +109,9 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
           }
         }
         ra[i] = v;
-      } else {    // rows m (BM) x k (BK) contiguous: float4 along k
-        const int m = idx / (BK / 4), k = 4 * (idx % (BK / 4));
+      } else {    // rows m (BM) x k (BK): float4 along k, consecutive lanes on consecutive m
+                  // (so the transposed LDS writes below are bank-conflict-free)
+        const int m = idx % BM, k = 4 * (idx / BM);
         const int64_t gk = k0 + k, gm = m0 + m;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (gm < g.M) {
@@ -100,8 +128,8 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < GLB; ++i) {
       const int idx = t + 256 * i;
-      if (TB) {   // B(k, n) = B[n·ldb + k]: float4 along k
-        const int n = idx / (BK / 4), k = 4 * (idx % (BK / 4));
+      if (TB) {   // B(k, n) = B[n·ldb + k]: float4 along k, consecutive lanes on consecutive n
+        const int n = idx % BN, k = 4 * (idx / BN);
         const int64_t gk = k0 + k, gn = n0 + n;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (gk + 3 < ke) {
@@ -120,6 +148,11 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
       }
     }
   };
+  const bool m_in = m0 + BM <= g.M;
+  auto gload = [&](int64_t k0) {
+    if (m_in && k0 + BK <= ke) gload_fast(k0);
+    else gload_edge(k0);
+  };
   // registers -> LDS image [k][m] / [k][n]
   auto lstore = [&](int buf) {
 #pragma unroll
@@ -129,7 +162,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
         const int k = idx / (BM / 4), m = 4 * (idx % (BM / 4));
         *reinterpret_cast<f32x4*>(&As[buf][k * LSA + m]) = ra[i];
       } else {
-        const int m = idx / (BK / 4), k = 4 * (idx % (BK / 4));
+        const int m = idx % BM, k = 4 * (idx / BM);
 #pragma unroll
         for (int e = 0; e < 4; ++e) As[buf][(k + e) * LSA + m] = ra[i][e];
       }
@@ -138,7 +171,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     for (int i = 0; i < GLB; ++i) {
       const int idx = t + 256 * i;
       if (TB) {
-        const int n = idx / (BK / 4), k = 4 * (idx % (BK / 4));
+        const int n = idx % BN, k = 4 * (idx / BN);
 #pragma unroll
         for (int e = 0; e < 4; ++e) Bs[buf][(k + e) * LS + n] = rb[i][e];
       } else {
@@ -168,19 +201,24 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     if (more) gload(kb + (int64_t)(c + 1) * BK);
     const float* as = As[buf];
     const float* bs = Bs[buf];
+    // all LDS operands of the chunk first (one latency exposed per chunk, not per k step)
+    float a[BK / 2][RB], b[BK / 2][2];
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
       const int kr = 2 * kk + kh;
-      float a[RB];
 #pragma unroll
-      for (int i = 0; i < RB; ++i) a[i] = as[kr * LSA + am + 32 * i];
-      const float b0 = bs[kr * LS + bn], b1 = bs[kr * LS + bn + 32];
+      for (int i = 0; i < RB; ++i) a[kk][i] = as[kr * LSA + am + 32 * i];
+      b[kk][0] = bs[kr * LS + bn];
+      b[kk][1] = bs[kr * LS + bn + 32];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk)
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b0, acc[i][0], 0, 0, 0);
-        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b1, acc[i][1], 0, 0, 0);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][0], acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][1], acc[i][1], 0, 0, 0);
       }
-    }
     if (more) lstore(buf ^ 1);
     __syncthreads();
   }

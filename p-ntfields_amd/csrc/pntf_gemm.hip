@@ -35,13 +35,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef PNTF_GEMM_BM
 #define PNTF_GEMM_BM 128
 #endif
-constexpr int BM = PNTF_GEMM_BM, BN = 128, BK = PNTF_GEMM_BK;
+constexpr int BM = PNTF_GEMM_BM, BN = 128, BK = PNTF_GEMM_BK;   // BN: the narrowest tile
 constexpr int RB = BM / 64;          // 32-row MFMA blocks per wave (waves are 2 x 2)
 constexpr int GLA = BM * BK / 1024;  // float4 global loads per lane per chunk: A
-constexpr int GLB = BN * BK / 1024;  //                                        B
 constexpr int LSA = BM + 32;         // LDS row strides (≡ 32 mod 64: conflict-free halves)
-constexpr int LS = 160;   // LDS row stride (floats): lanes 32-63 read the next k row in the
-                          // other 32 banks (stride ≡ 32 mod 64), conflict-free
 
 struct GemmArgs {
   const float* A;
@@ -52,15 +49,18 @@ struct GemmArgs {
   float beta;
 };
 
-template <bool TA, bool TB>
+template <bool TA, bool TB, int BNT>
 __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
+  constexpr int GLB = BNT * BK / 1024;   // float4 global loads per lane per chunk: B
+  constexpr int LSB = BNT + 32;          // ≡ 32 mod 64, like LSA
+  constexpr int CB = BNT / 64;           // 32-column MFMA blocks per wave
   __shared__ float As[2][BK * LSA];
-  __shared__ float Bs[2][BK * LS];
+  __shared__ float Bs[2][BK * LSB];
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w & 1, wn = w >> 1;
   const int64_t m0 = (int64_t)blockIdx.y * BM;
-  const int64_t n0 = (int64_t)blockIdx.x * BN;
+  const int64_t n0 = (int64_t)blockIdx.x * BNT;
   const int64_t kb = (int64_t)blockIdx.z * g.kper;
   const int64_t ke = kb + g.kper < g.K ? kb + g.kper : g.K;
   const int nchunks = (int)((ke - kb + BK - 1) / BK);
@@ -84,10 +84,10 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     for (int i = 0; i < GLB; ++i) {
       const int idx = t + 256 * i;
       if (TB) {
-        const int n = idx % BN, k = 4 * (idx / BN);
+        const int n = idx % BNT, k = 4 * (idx / BNT);
         rb[i] = *reinterpret_cast<const f32x4*>(g.B + (n0 + n) * g.ldb + k0 + k);
       } else {
-        const int k = idx >> 5, n = 4 * (idx & 31);
+        const int k = idx / (BNT / 4), n = 4 * (idx % (BNT / 4));
         rb[i] = *reinterpret_cast<const f32x4*>(g.B + (k0 + k) * g.ldb + n0 + n);
       }
     }
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     for (int i = 0; i < GLB; ++i) {
       const int idx = t + 256 * i;
       if (TB) {   // B(k, n) = B[n·ldb + k]: float4 along k, consecutive lanes on consecutive n
-        const int n = idx % BN, k = 4 * (idx / BN);
+        const int n = idx % BNT, k = 4 * (idx / BNT);
         const int64_t gk = k0 + k, gn = n0 + n;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (gk + 3 < ke) {
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
         }
         rb[i] = v;
       } else {    // B(k, n) = B[k·ldb + n]: float4 along n
-        const int k = idx >> 5, n = 4 * (idx & 31);
+        const int k = idx / (BNT / 4), n = 4 * (idx % (BNT / 4));
         const int64_t gk = k0 + k;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (gk < ke) v = *reinterpret_cast<const f32x4*>(g.B + gk * g.ldb + n0 + n);
@@ -171,21 +171,21 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     for (int i = 0; i < GLB; ++i) {
       const int idx = t + 256 * i;
       if (TB) {
-        const int n = idx % BN, k = 4 * (idx / BN);
+        const int n = idx % BNT, k = 4 * (idx / BNT);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Bs[buf][(k + e) * LS + n] = rb[i][e];
+        for (int e = 0; e < 4; ++e) Bs[buf][(k + e) * LSB + n] = rb[i][e];
       } else {
-        const int k = idx >> 5, n = 4 * (idx & 31);
-        *reinterpret_cast<f32x4*>(&Bs[buf][k * LS + n]) = rb[i];
+        const int k = idx / (BNT / 4), n = 4 * (idx % (BNT / 4));
+        *reinterpret_cast<f32x4*>(&Bs[buf][k * LSB + n]) = rb[i];
       }
     }
   };
 
-  f32x16 acc[RB][2];
+  f32x16 acc[RB][CB];
 #pragma unroll
   for (int i = 0; i < RB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < CB; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     lstore(0);
   }
   __syncthreads();
-  const int am = wm * (BM / 2) + (lane & 31), bn = wn * 64 + (lane & 31), kh = lane >> 5;
+  const int am = wm * (BM / 2) + (lane & 31), bn = wn * (BNT / 2) + (lane & 31), kh = lane >> 5;
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
     const bool more = c + 1 < nchunks;
@@ -202,23 +202,23 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
     const float* as = As[buf];
     const float* bs = Bs[buf];
     // all LDS operands of the chunk first (one latency exposed per chunk, not per k step)
-    float a[BK / 2][RB], b[BK / 2][2];
+    float a[BK / 2][RB], b[BK / 2][CB];
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
       const int kr = 2 * kk + kh;
 #pragma unroll
       for (int i = 0; i < RB; ++i) a[kk][i] = as[kr * LSA + am + 32 * i];
-      b[kk][0] = bs[kr * LS + bn];
-      b[kk][1] = bs[kr * LS + bn + 32];
+#pragma unroll
+      for (int j = 0; j < CB; ++j) b[kk][j] = bs[kr * LSB + bn + 32 * j];
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < RB; ++i) {
-        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][0], acc[i][0], 0, 0, 0);
-        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][1], acc[i][1], 0, 0, 0);
-      }
+      for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < CB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
     if (more) lstore(buf ^ 1);
     __syncthreads();
   }
@@ -228,11 +228,11 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(GemmArgs g) {
 #pragma unroll
   for (int i = 0; i < RB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < CB; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = m0 + wm * (BM / 2) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        const int64_t col = n0 + wn * 64 + 32 * j + (lane & 31);
+        const int64_t col = n0 + wn * (BNT / 2) + 32 * j + (lane & 31);
         if (row < g.M) {
           if (split) {
             g.work[((int64_t)blockIdx.z * g.M + row) * g.N + col] = acc[i][j][r];
@@ -284,8 +284,17 @@ int num_cus() {
 }
 
 // Split-K factor: enough workgroups for 2 per CU, chunks of at least 1024 rows of K.
+// Tile width: 128 columns.  256 (the A panel read once per row tile, PNTF_GEMM_WIDE=1) halves
+// the occupancy and measured 10-20 % slower on the training shapes (tests/diag/gemm_variants.py).
+#ifndef PNTF_GEMM_WIDE
+#define PNTF_GEMM_WIDE 0
+#endif
+int tile_n(int64_t M, int64_t N) {
+  return PNTF_GEMM_WIDE && N % 256 == 0 && (M + BM - 1) / BM >= 2 * (int64_t)num_cus() ? 256 : 128;
+}
+
 int64_t splits_for(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ((M + BM - 1) / BM) * (N / BN);
+  const int64_t tiles = ((M + BM - 1) / BM) * (N / tile_n(M, N));
   int64_t s = (2 * (int64_t)num_cus() + tiles - 1) / tiles;
   const int64_t kmax = (K + 1023) / 1024;
   if (s > kmax) s = kmax;
@@ -325,11 +334,19 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
   GemmArgs g{A, B, C, work, M, N, K, lda, ldb, ldc, 0, beta};
   g.kper = ((K + s - 1) / s + BK - 1) / BK * BK;
   if (g.kper < BK) g.kper = BK;
-  dim3 grid((unsigned)(N / BN), (unsigned)((M + BM - 1) / BM), (unsigned)s), block(256);
-  if (ta && tb) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, stream, g);
-  else if (ta) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, block, 0, stream, g);
-  else if (tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, block, 0, stream, g);
-  else hipLaunchKernelGGL((gemm_kernel<false, false>), grid, block, 0, stream, g);
+  const int bn = tile_n(M, N);
+  dim3 grid((unsigned)(N / bn), (unsigned)((M + BM - 1) / BM), (unsigned)s), block(256);
+  if (bn == 256) {
+    if (ta && tb) hipLaunchKernelGGL((gemm_kernel<true, true, 256>), grid, block, 0, stream, g);
+    else if (ta) hipLaunchKernelGGL((gemm_kernel<true, false, 256>), grid, block, 0, stream, g);
+    else if (tb) hipLaunchKernelGGL((gemm_kernel<false, true, 256>), grid, block, 0, stream, g);
+    else hipLaunchKernelGGL((gemm_kernel<false, false, 256>), grid, block, 0, stream, g);
+  } else {
+    if (ta && tb) hipLaunchKernelGGL((gemm_kernel<true, true, 128>), grid, block, 0, stream, g);
+    else if (ta) hipLaunchKernelGGL((gemm_kernel<true, false, 128>), grid, block, 0, stream, g);
+    else if (tb) hipLaunchKernelGGL((gemm_kernel<false, true, 128>), grid, block, 0, stream, g);
+    else hipLaunchKernelGGL((gemm_kernel<false, false, 128>), grid, block, 0, stream, g);
+  }
   if (s > 1) {
     const int64_t n = M * N;
     const unsigned nb = (unsigned)((n + 255) / 256);

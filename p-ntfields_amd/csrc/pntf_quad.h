@@ -33,6 +33,9 @@ constexpr int QPAIRS = 4;
 #define PNTF_Q_CHAINS 2
 #endif
 constexpr int QCH = PNTF_Q_CHAINS;
+#ifndef PNTF_QKEEPB
+#define PNTF_QKEEPB 1
+#endif
 // Fragments in flight per wave: the ∇τ kernels (1056 fragments per step, a multiple of 32)
 // run PNTF_QRING of them; the τ-only kernels wrap every 528 fragments and run 16.
 #ifndef PNTF_QRING
@@ -129,7 +132,18 @@ template <int NC, int IN, int NF, int G, int S0, int QR, class Epi>
 __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, const lds_f* in,
                                        Epi&& epi) {
   constexpr int SP = IN / 4 + 4, NQ = IN / 16;
+  // B operands kept in registers for all groups of the layer when they fit (64 VGPRs):
+  // one LDS read per fragment instead of one per fragment and group
+  constexpr bool KEEP = PNTF_QKEEPB && G > 1 && NC * NQ <= 16;
   const lds_f* src = in + cx.l16 * SP;
+  f32x4 xb[KEEP ? NC : 1][KEEP ? NQ : 1];
+  if constexpr (KEEP) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        xb[c][q] = *reinterpret_cast<const lds_f4*>(src + c * 16 * SP + 4 * q);
+  }
   static_for<0, G>([&](auto gg) {
     constexpr int g = decltype(gg)::value;
     f32x4 acc[NC][QCH];
@@ -145,7 +159,8 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
 #ifdef PNTF_QABL_NOLDS   // diagnostics only (tests/diag timing ablations; wrong results)
         b[c] = f32x4{0.1f * q, 0.2f * c, 0.3f, 0.4f} + (float)cx.lane;
 #else
-        b[c] = *reinterpret_cast<const lds_f4*>(src + c * 16 * SP + 4 * q);
+        if constexpr (KEEP) b[c] = xb[c][q];
+        else b[c] = *reinterpret_cast<const lds_f4*>(src + c * 16 * SP + 4 * q);
 #endif
       }
       const f32x4 a = ring.r[slot];

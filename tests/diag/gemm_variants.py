@@ -55,7 +55,12 @@ def main(names, pairs=20000):
             f()
             torch.cuda.synchronize()
             assert (Y - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
-            res[tag + "_bwdx"] = round(fl / timeit(run(GX, G, W, 0, 0, rows, K, N)), 1)
+            f = run(GX, G, W, 0, 0, rows, K, N)
+            res[tag + "_bwdx"] = round(fl / timeit(f), 1)
+            ref = G @ W
+            f()
+            torch.cuda.synchronize()
+            assert (GX - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
             res[tag + "_bwdw"] = round(fl / timeit(run(GW, G, X, 1, 0, N, K, rows)), 1)
         print(name, res, flush=True)
 

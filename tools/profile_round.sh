@@ -12,9 +12,10 @@ BENCH="$R/bench.py --no-cpu --no-extra --roofline-launches 1"
 run() {  # run <dir> <seconds> <rocprofv3 args...>
   local d=$1 t=$2; shift 2
   timeout -k 10 "$t" rocprofv3 "$@" -d "$OUT/$d" -o run --output-format csv -- \
-    python3 $BENCH --steps 3 --warmup 1 > "$OUT/$d.log" 2>&1
+    python3 $BENCH --steps ${STEPS:-3} --warmup 1 > "$OUT/$d.log" 2>&1
 }
-run prof_stats 300 --kernel-trace --stats
+# the stats pass times 20 steps, so the one cold first launch weighs 1/27 of the mean
+STEPS=20 run prof_stats 300 --kernel-trace --stats
 run pmc_fetch 300 --pmc FETCH_SIZE
 run pmc_write 300 --pmc WRITE_SIZE
 run pmc_mfma 300 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES

@@ -224,6 +224,14 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
                  size_t work_floats, hipStream_t stream);
 const char* pntf_tt_gemm_last_error(void);
 
+/* A forward Linear of the Taylor tape fused with pntf_tt_act_fwd (ndir = 3 | 6, R = 1 + 2*ndir
+ * planes): y (R, m, n) = x (R, m, k) · Wᵀ (W: n x k), y's value plane += bias, every plane +=
+ * res (R, m, n) when res is not NULL; act != 0: h (R, m, n) = softplus10 Taylor rows of y.
+ * k a multiple of 16, n a multiple of 128.  Errors: pntf_tt_gemm_last_error. */
+int pntf_tt_linear_act(int ndir, const float* x, int64_t m, int k, const float* w, int n,
+                       const float* bias, const float* res, int act, float* y, float* h,
+                       hipStream_t stream);
+
 /* torch.optim.AdamW update of one parameter tensor (the reference's optimizer, :959-961):
  * p, grad, exp_avg, exp_avg_sq (n); `step` = the step count after this update (>= 1). */
 int pntf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,

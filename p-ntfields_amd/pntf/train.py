@@ -103,10 +103,11 @@ class _Tape:
     """Forward tape of one loss evaluation: (name, input planes, pre-activation planes, act,
     has_residual) per Linear, in execution order."""
 
-    def __init__(self, params, dim, device):
+    def __init__(self, params, dim, device, fused=False):
         self.p = params
         self.dim = dim
         self.dev = device
+        self.fused = fused
         self.s = _stream(device)
         self.lib = _lib.load()
         self.ops = []
@@ -115,11 +116,21 @@ class _Tape:
         W, b = self.p[name + ".weight"], self.p[name + ".bias"]
         R, M, K = x3.shape
         N = W.shape[0]
+        ndir = (R - 1) // 2
         y = torch.empty((R, M, N), dtype=torch.float32, device=self.dev)
-        gemm(y.view(R * M, N), x3.view(R * M, K), W, ta=False, tb=True)
         h = torch.empty_like(y) if act else None
-        check(self.lib.pntf_tt_act_fwd((R - 1) // 2, _vp(y), _vp(h), _vp(b), _vp(res), M, N,
-                                       int(act), self.s), "pntf_tt_act_fwd")
+        if self.fused and ndir in (3, 6):
+            # GEMM + bias/residual/act_laplace in one kernel (32 points x all planes per tile);
+            # off by default: it measured slower than the two passes
+            st = self.lib.pntf_tt_linear_act(ndir, _vp(x3), M, K, _vp(W), N, _vp(b), _vp(res),
+                                             int(act), _vp(y), _vp(h), self.s)
+            if st != 0:
+                raise PntfError("pntf_tt_linear_act: " +
+                                self.lib.pntf_tt_gemm_last_error().decode())
+        else:
+            gemm(y.view(R * M, N), x3.view(R * M, K), W, ta=False, tb=True)
+            check(self.lib.pntf_tt_act_fwd(ndir, _vp(y), _vp(h), _vp(b), _vp(res), M, N,
+                                           int(act), self.s), "pntf_tt_act_fwd")
         self.ops.append((name, x3, y, act, res is not None))
         return h if act else y
 
@@ -131,7 +142,7 @@ def weight_grad(g2, x2, out):
     gemm(out, g2, x2, ta=True, tb=False)
 
 
-def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
+def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads, fused=False):
     """diff (n,) of Model.Loss and, into `grads` (key -> tensor shaped like the parameter),
     the gradient of scale·Σ diff w.r.t. every trained parameter.
 
@@ -144,7 +155,7 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
         for g in grads.values():
             g.zero_()
         return torch.empty(0, dtype=torch.float32, device=dev)
-    tape = _Tape(params, dim, dev)
+    tape = _Tape(params, dim, dev, fused)
     s = tape.s
     Re, Rg = 1 + 2 * dim, 1 + 4 * dim
     phi = torch.empty((Re, 2 * n, 2 * H), dtype=torch.float32, device=dev)

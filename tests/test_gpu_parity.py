@@ -351,3 +351,29 @@ def test_device_sum_deterministic(dev):
     a, b = ops.device_sum(x), ops.device_sum(x)
     assert a.item() == b.item()
     assert abs(a.item() - float(x.double().sum())) < 1e-6 * float(x.abs().sum())
+
+
+@pytest.mark.parametrize("schedule", ["wave_tile", "split_tile", "quad_tile"])
+def test_planner_edge_cases(packed, dev, schedule, W):
+    """Loop-cap semantics (at most max_iter + 1 updates, test/gib_plan.py:83-86), max_iter 0,
+    queries already within tol (0 steps, constant path), an invalid env id (steps -1), a
+    ragged batch of 5 — every schedule against the oracle."""
+    q = 5
+    xp0 = synth.make_pairs(q, 3, seed=11)
+    xp0[1, 3:] = xp0[1, :3] + 0.001            # already converged: |xg - xs| < tol
+    B1 = synth.make_B(3, seed=1)
+    Bt = np.stack([B1, synth.make_B(3, seed=2)])
+    env = np.array([0, 1, 0, 7, 1], np.int32)   # env 7 does not exist
+    for max_iter in (3, 0):
+        path, steps = ops.plan(packed, T(xp0, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3,
+                               step=1e-4, tol=0.06, max_iter=max_iter,
+                               mode=ops.GRAD_BACKGRAD_COMPAT, schedule=schedule)
+        path, steps = path.cpu().numpy(), steps.cpu().numpy()
+        assert path.shape == (q, max_iter + 2, 6)
+        assert steps[3] == -1
+        assert steps[1] == 0 and np.all(path[1] == xp0[1])
+        for i in (0, 2, 4):
+            po, so = O.plan(W, xp0[i:i + 1], Bt[env[i]], step=1e-4, tol=0.06,
+                            max_iter=max_iter, compat=True)
+            assert steps[i] == so[0] == max_iter + 1
+            assert np.abs(path[i] - po[0]).max() < 1e-5

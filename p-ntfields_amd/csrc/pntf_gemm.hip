@@ -416,12 +416,17 @@ __global__ __launch_bounds__(256, 1) void tt_linear_act_kernel(LinArgs a) {
 
 thread_local char g_err[512] = "";
 
+// CU count of the current device, cached per device (queried on every GEMM otherwise).
 int num_cus() {
-  int dev = 0, cus = 0;
+  static int cache[64] = {};
+  int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev >= 0 && dev < 64 && cache[dev] > 0) return cache[dev];
+  int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
     return 256;
+  if (dev >= 0 && dev < 64) cache[dev] = cus;
   return cus;
 }
 

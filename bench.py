@@ -371,10 +371,15 @@ def extras(packed, dev):
     out["c5_arm_plan_mean_steps"] = float(steps.mean())
     out["c5_arm_plan_max_steps"] = int(steps.max())
     out["c5_arm_plan_1024q_wave_tile_ms"] = timeit(lambda: run_plan("wave_tile"), reps=2)
+    out["c5_arm_plan_1024q_split_tile_ms"] = timeit(lambda: run_plan("split_tile"), reps=2)
+    # the quad planner's C5 step time and its roofline: a step streams both weight directions
+    # (4.33 MB) through each tile's CU; the measured per-CU stream floor is ~42 us
+    # (tests/diag/stream_probe.hip), the 4x4x1 MFMA work ~23 us
+    out["c5_arm_plan_us_per_step"] = 1e3 * ms / max(int(steps.max()), 1)
     # batch-1 Gibson planner (test/gib_plan.py runs Q = 1): device time per loop step
     x1 = torch.from_numpy(synth.make_pairs(1, 3, seed=21)).to(dev)
     B1 = torch.from_numpy(synth.make_B(3, seed=1)).to(dev)
-    for sched in ("auto", "wave_tile"):
+    for sched in ("auto", "split_tile", "wave_tile"):
         def run1():
             res["p1"] = ops.plan(packed, x1, B1, dim=3, step=0.03, tol=1e-9, max_iter=99,
                                  mode=ops.GRAD_BACKGRAD_COMPAT, schedule=sched)

@@ -18,6 +18,8 @@
 // to `work` and a second kernel sums them in split order: deterministic, no atomics.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdint.h>
+#include <stdlib.h>
 
 #include "pntf.h"
 
@@ -273,6 +275,166 @@ __global__ void gemm_reduce2_kernel(const float* __restrict__ work, int splits, 
 }
 
 // ---------------------------------------------------------------------------------------
+// Panel GEMM: the forward X·Wᵀ and the input gradient gY·W of every Linear (K, N ∈ {128, 256}).
+//   C (M x NC) = (C +) A (M x KC) · B,   B (KC x NC) = the layer weight, Wᵀ or W.
+// The field kernels' transposed formulation (pntf_wide.h) applied to the tape: one wave owns a
+// 32-row panel of A held in registers (KC/8 float4 per lane, read from HBM once), and the
+// weight is the streamed MFMA A operand, pre-packed in fragment order (1 KiB per wave load,
+// L2-resident), so there is no LDS, no barrier and no B-tile re-read:
+//   D (32 out cols x 32 rows) += Bᵀfrag (32 x 2) · panelᵀ (2 x 32) per v_mfma_f32_32x32x2_f32.
+// MFMA step s = 4q + e, lane half h, uses K index k = 8q + 4h + e: lane (row j, half h) holds
+// A[row j][8q + 4h .. +3] as one float4 (x[q]) and the packed fragment
+//   P[((nt·QK + q)·64 + lane)·4 + e] = B(8q + 4h + e, 32·nt + (lane & 31))
+// supplies out column 32·nt + (lane & 31).  D register r of lane (j, h) is C[row j][32·nt +
+// 8·(r >> 2) + 4h + (r & 3)]: four float4 stores per 32-column tile.
+// Per tile: NC/128 groups of 4 out tiles (64 accumulators) x KC/8 iterations of 16 MFMAs; a
+// 4-slot register ring prefetches fragments 3 iterations ahead and wraps into the next tile
+// (the stream is the same for every tile).  The next panel's float4 q is loaded right after
+// its last use in the last group, so the panel double-buffers in place.  Persistent waves,
+// one per SIMD (≤ 512 VGPRs), grid-stride over 32-row tiles.  ACC adds C (the residual
+// branch's gradient, beta = 1), loaded 4 iterations before the group's store.
+#ifndef PNTF_PANEL_PF
+#define PNTF_PANEL_PF 3
+#endif
+// diagnostic builds only (tests/diag/panel_variants.py): bit 1 = no next-panel loads (every
+// tile reuses the first panel), bit 2 = no C stores, bit 4 = no fragment loads (ring reuse)
+// waves per SIMD (workgroups per CU): 1 keeps ≤ 512 registers per wave
+#ifndef PNTF_PANEL_WPS
+#define PNTF_PANEL_WPS 1
+#endif
+#ifndef PNTF_PANEL_DIAG
+#define PNTF_PANEL_DIAG 0
+#endif
+template <int B, int E, class F>
+__device__ __forceinline__ void pg_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    pg_static_for<B + 1, E>(f);
+  }
+}
+
+struct PanelArgs {
+  const float* A;
+  const f32x4* P;
+  float* C;
+  int64_t M, lda, ldc;
+};
+
+__global__ void panel_pack_kernel(const float* __restrict__ W, int64_t ldb, int tb, int KC,
+                                  int NC, f32x4* __restrict__ P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int QK = KC / 8;
+  if (i >= (int64_t)(NC / 32) * QK * 64) return;
+  const int lane = (int)(i & 63), q = (int)((i >> 6) % QK), nt = (int)((i >> 6) / QK);
+  const int n = 32 * nt + (lane & 31), k0 = 8 * q + 4 * (lane >> 5);
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = tb ? W[(int64_t)n * ldb + k0 + e] : W[(int64_t)(k0 + e) * ldb + n];
+  P[i] = v;
+}
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+// Buffer resources keep the per-load address math on the SALU (scalar fragment / column
+// offsets) and clip the M edge: loads past num_records return 0, stores there are dropped.
+__device__ __forceinline__ Rsrc pg_rsrc(const float* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 pg_load(Rsrc r, int voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void pg_store(Rsrc r, f32x4 v, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                         r, voff, soff, 0);
+}
+
+template <int KC, int NC, bool ACC>
+__global__ __launch_bounds__(256, PNTF_PANEL_WPS) void panel_gemm_kernel(PanelArgs g) {
+  constexpr int QK = KC / 8, NG = NC / 128, NQ = NG * QK, PF = PNTF_PANEL_PF, NS = PF + 1;
+  static_assert(NQ % NS == 0, "ring slots must divide the per-tile fragment stream");
+  static_assert(QK >= 8, "C prefetch distance");
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int64_t ntiles = (g.M + 31) / 32;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t tile = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (tile >= ntiles) return;   // wave-uniform
+  // the 32-row window of tile t in A / C (rows past M are outside the resource)
+  auto win = [&](const float* base, int64_t ld, int64_t t) {
+    const int64_t rows = g.M - 32 * t;
+    return pg_rsrc(base + 32 * t * ld, (rows < 32 ? rows : 32) * ld * 4);
+  };
+  const int va = (int)((j * g.lda + 4 * h) * 4), vc = (int)((j * g.ldc + 4 * h) * 4);
+  const Rsrc rp = pg_rsrc(reinterpret_cast<const float*>(g.P), (int64_t)KC * NC * 4);
+  const int vp = lane * 16;
+  f32x4 x[QK];
+  {
+    const Rsrc ra = win(g.A, g.lda, tile);
+#pragma unroll
+    for (int q = 0; q < QK; ++q) x[q] = pg_load(ra, va, 32 * q);
+  }
+  f32x4 ring[NS][4];
+  pg_static_for<0, PF>([&](auto I) {
+    constexpr int it = decltype(I)::value;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ring[it][t] = pg_load(rp, vp, ((4 * (it / QK) + t) * QK + it % QK) * 1024);
+  });
+  for (;;) {
+    const int64_t next = tile + stride;
+    const bool more = next < ntiles;
+    const Rsrc rn = win(g.A, g.lda, more ? next : tile);
+    const Rsrc rc = win(g.C, g.ldc, tile);
+    f32x16 acc[4];
+    f32x4 cb[4][4];
+    pg_static_for<0, NQ>([&](auto I) {
+      constexpr int it = decltype(I)::value, G = it / QK, q = it % QK;
+      if constexpr (q == 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+      }
+      if constexpr (ACC && q == QK - 4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int R = 0; R < 4; ++R) cb[t][R] = pg_load(rc, vc, (32 * (4 * G + t) + 8 * R) * 4);
+      }
+      // prefetch PF iterations ahead; past the tile's end the stream wraps to the next tile
+      constexpr int pit = (it + PF) % NQ;
+      if constexpr (!(PNTF_PANEL_DIAG & 4)) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          ring[(it + PF) % NS][t] = pg_load(rp, vp, ((4 * (pit / QK) + t) * QK + pit % QK) * 1024);
+      }
+      // four independent accumulator chains per k step; the fence keeps the scheduler from
+      // regrouping them into back-to-back dependent MFMAs (it orders by load arrival)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(ring[it % NS][t][e], x[q][e], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (G == NG - 1 && !(PNTF_PANEL_DIAG & 1)) {
+        if (more) x[q] = pg_load(rn, va, 32 * q);   // x[q] is dead for this tile: next panel
+      }
+      if constexpr (q == QK - 1 && !(PNTF_PANEL_DIAG & 2)) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int R = 0; R < 4; ++R) {
+            f32x4 v = {acc[t][4 * R], acc[t][4 * R + 1], acc[t][4 * R + 2], acc[t][4 * R + 3]};
+            if (ACC) v += cb[t][R];
+            pg_store(rc, v, vc, (32 * (4 * G + t) + 8 * R) * 4);
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (!more) break;
+    tile = next;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Forward Linear of the Taylor tape fused with its epilogue (pntf_tt_linear_act): per point
 // and feature, y planes = x planes · Wᵀ, y₀ += bias, (+ residual planes), then act_laplace
 // (:675-691) h₀ = softplus₁₀(y₀), h_J = σ·J, h_L = σ'·J² + σ·L — the work of pntf_tt_gemm +
@@ -449,6 +611,20 @@ int64_t splits_for(int64_t M, int64_t N, int64_t K) {
   return s < 1 ? 1 : s;
 }
 
+// The panel path serves the forward / input-gradient shapes: K, N ∈ {128, 256}, dense rows,
+// beta 0 or 1, 16-byte aligned operands.  PNTF_GEMM_PANEL=0 in the environment turns it off
+// (the LDS-tiled kernel then runs every shape; used to compare the two).
+bool panel_shape(int64_t N, int64_t K) {
+  return (K == 128 || K == 256) && (N == 128 || N == 256);
+}
+bool panel_enabled() {
+  static const int on = [] {
+    const char* e = getenv("PNTF_GEMM_PANEL");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 }  // namespace pntf_gemm
 
 using namespace pntf_gemm;
@@ -458,7 +634,9 @@ extern "C" {
 size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const int64_t s = splits_for(M, N, K);
-  return s > 1 ? (size_t)(s * M * N) : 0;
+  const size_t split = s > 1 ? (size_t)(s * M * N) : 0;
+  const size_t packed = panel_shape(N, K) ? (size_t)(K * N) : 0;
+  return split > packed ? split : packed;
 }
 
 int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
@@ -472,6 +650,32 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
   if (!A || !B || !C) {
     snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: null pointer");
     return PNTF_ERR_ARG;
+  }
+  if (!ta && (beta == 0.f || beta == 1.f) && panel_shape(N, K) && panel_enabled() &&
+      lda == K && ldc == N && work && work_floats >= (size_t)(K * N) &&
+      ((uintptr_t)A & 15) == 0 && ((uintptr_t)C & 15) == 0 && ((uintptr_t)work & 15) == 0) {
+    const int64_t nf = (N / 32) * (K / 8) * 64;
+    hipLaunchKernelGGL(panel_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0,
+                       stream, B, ldb, tb, (int)K, (int)N, reinterpret_cast<f32x4*>(work));
+    PanelArgs p{A, reinterpret_cast<const f32x4*>(work), C, M, lda, ldc};
+    const int64_t tiles = (M + 31) / 32, wgs = (tiles + 3) / 4;
+    const int64_t slots = (int64_t)PNTF_PANEL_WPS * num_cus();
+    const unsigned grid = (unsigned)(wgs < slots ? wgs : slots);
+#define PNTF_PANEL(KC, NC)                                                                     \
+  if (beta != 0.f) hipLaunchKernelGGL((panel_gemm_kernel<KC, NC, true>), dim3(grid), dim3(256), \
+                                      0, stream, p);                                           \
+  else hipLaunchKernelGGL((panel_gemm_kernel<KC, NC, false>), dim3(grid), dim3(256), 0, stream, p);
+    if (K == 128 && N == 128) { PNTF_PANEL(128, 128) }
+    else if (K == 128) { PNTF_PANEL(128, 256) }
+    else if (N == 128) { PNTF_PANEL(256, 128) }
+    else { PNTF_PANEL(256, 256) }
+#undef PNTF_PANEL
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: %s", hipGetErrorString(e));
+      return PNTF_ERR_HIP;
+    }
+    return PNTF_OK;
   }
   const int64_t s = K > 0 ? splits_for(M, N, K) : 1;
   if (s > 1 && (!work || work_floats < (size_t)(s * M * N))) {

@@ -150,11 +150,21 @@ def _resources(stderr):
     return out
 
 
-def _compile(unit):
+def _compile(unit, uid=None):
     name, src, defs = unit
     d = os.path.join(BUILD, name)
     os.makedirs(d, exist_ok=True)
     obj = os.path.join(d, name + ".o")
+    # per-unit cache: a unit whose code identity (and, for capi, the whole build-info string)
+    # is unchanged since its last successful compile is not rebuilt
+    key = None if uid is None else uid + (
+        "" if name != "capi" else repr(sorted(unit_ids().items())))
+    idp = os.path.join(d, "unit.id")
+    if uid is not None and os.path.exists(obj) and os.path.exists(idp):
+        with open(idp) as fh:
+            prev = json.load(fh)
+        if prev.get("id") == key:
+            return obj, prev.get("res", {})
     if name == "capi":
         defs = defs + ['-DPNTF_BUILD_INFO="%s"' % ";".join(
             "%s=%s" % kv for kv in sorted(unit_ids().items()))]
@@ -187,7 +197,11 @@ def _compile(unit):
     for f in glob.glob(os.path.join(d, "*")):
         if not f.endswith((".o", ".s")):
             os.remove(f)
-    return obj, {name + ":" + k: v for k, v in res.items()}
+    out = {name + ":" + k: v for k, v in res.items()}
+    if uid is not None:
+        with open(idp, "w") as fh:
+            json.dump({"id": key, "res": out}, fh)
+    return obj, out
 
 
 def build(jobs=None, force=False, verbose=True):
@@ -203,8 +217,9 @@ def build(jobs=None, force=False, verbose=True):
     jobs = jobs or min(len(UNITS), max(1, min(16, os.cpu_count() or 1)))
     if verbose:
         print("building libpntf.so (%d units, %d jobs, %s)" % (len(UNITS), jobs, ARCH))
+    ids = unit_ids()
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(_compile, UNITS))
+        results = list(ex.map(lambda u: _compile(u, None if force else ids[u[0]]), UNITS))
     objs = [o for o, _ in results]
     report = {}
     for _, res in results:

@@ -388,7 +388,8 @@ def test_mfma_gemm_vs_fp64(ta, tb, M, N, K, beta):
 @pytest.mark.gpu
 def test_training_uses_no_vendor_gemm():
     """The training step's GEMMs are the library's own MFMA kernels: a profiled
-    Loss + backward launches gemm_kernel and no Tensile (Cijk_*) / hipBLASLt kernel."""
+    Loss + backward launches gemm_kernel (weight gradients) and panel_gemm_kernel (forward,
+    input gradients) and no Tensile (Cijk_*) / hipBLASLt kernel."""
     from torch.profiler import ProfilerActivity, profile
     dev = torch.device("cuda:0")
     f = load("train_d3.npz")
@@ -402,6 +403,8 @@ def test_training_uses_no_vendor_gemm():
         torch.cuda.synchronize()
     names = [e.key for e in prof.key_averages()]
     assert any("gemm_kernel" in n for n in names), names
+    # forward / input-gradient Linears run on the register-panel kernel
+    assert any("panel_gemm_kernel" in n for n in names), names
     assert not any("Cijk" in n or "hipblaslt" in n.lower() for n in names), names
 
 

@@ -86,9 +86,18 @@ def mfma_probe(pairs=20000):
              "fwd_torch": fl / timeit(lambda: torch.mm(X, W.t(), out=Y)),
              "bwdx": fl / timeit(lambda: gemm(GX, G, W, False, False)),
              "bwdx_torch": fl / timeit(lambda: torch.mm(G, W, out=GX)),
+             "bwdx_acc": fl / timeit(lambda: gemm(GX, G, W, False, False, 1.0)),
              "bwdw": fl / timeit(lambda: gemm(GW, G, X, True, False)),
              "bwdw_torch": fl / timeit(lambda: torch.mm(G.t(), X, out=GW))}
-        out[tag] = {k: round(v, 1) for k, v in r.items()}
+        gemm(Y, X, W, False, True)
+        ref = X.double() @ W.double().t()
+        r["fwd_err"] = ((Y.double() - ref).abs().max() / ref.abs().max()).item()
+        GX.copy_(X if K == X.shape[1] else GX)
+        C0 = GX.clone()
+        gemm(GX, G, W, False, False, 1.0)
+        ref = C0.double() + G.double() @ W.double()
+        r["bwdx_acc_err"] = ((GX.double() - ref).abs().max() / ref.abs().max()).item()
+        out[tag] = {k: (round(v, 1) if v > 1e-3 else v) for k, v in r.items()}
     print(json.dumps(out, indent=1))
 
 

@@ -592,7 +592,7 @@ int num_cus() {
   return cus;
 }
 
-// Split-K factor: enough workgroups for 2 per CU, chunks of at least 1024 rows of K.
+// Split-K factor: enough workgroups for 2 per CU, chunks of at least 512 rows of K.
 // Tile width: 128 columns.  256 (the A panel read once per row tile, PNTF_GEMM_WIDE=1) halves
 // the occupancy and measured 10-20 % slower on the training shapes (tests/diag/gemm_variants.py).
 #ifndef PNTF_GEMM_WIDE
@@ -605,9 +605,13 @@ int tile_n(int64_t M, int64_t N) {
 int64_t splits_for(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + BM - 1) / BM) * (N / tile_n(M, N));
   int64_t s = (2 * (int64_t)num_cus() + tiles - 1) / tiles;
-  const int64_t kmax = (K + 1023) / 1024;
+  const int64_t kmax = (K + 511) / 512;
   if (s > kmax) s = kmax;
   if (s > PNTF_GEMM_SPLITS) s = PNTF_GEMM_SPLITS;
+  // whole waves of workgroups: 273 splits of a 128x128 gradient put a second workgroup on 17
+  // CUs and doubled the kernel's time; round the grid down to a multiple of the CU count
+  const int64_t cus = num_cus();
+  if (tiles * s > cus) s = (tiles * s / cus) * cus / tiles;
   return s < 1 ? 1 : s;
 }
 

@@ -217,7 +217,11 @@ int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const f
  * C (M x N, row stride ldc) = beta*C + A·B with A(m,k) = ta ? A[k*lda + m] : A[m*lda + k] and
  * B(k,n) = tb ? B[n*ldb + k] : B[k*ldb + n].  N must be a multiple of 128.  Long K is split
  * over workgroups (deterministic partial sums in `work`, pntf_tt_gemm_work_floats(M, N, K)
- * floats; may be NULL when that is 0).  beta == 0 never reads C. */
+ * floats; may be NULL when that is 0).  beta == 0 never reads C.  With ta == 0, K and N in
+ * {128, 256}, dense rows (lda == K, ldc == N), beta 0 or 1 and 16-byte aligned A, C and work,
+ * the register-panel kernel runs: it packs op(B) into `work` (K*N floats, which
+ * pntf_tt_gemm_work_floats includes) and streams it; otherwise the LDS-tiled kernel.  Setting
+ * PNTF_GEMM_PANEL=0 in the environment (read once) disables the panel kernel. */
 size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K);
 int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                  const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,

@@ -1,6 +1,7 @@
 // C ABI of libpntf.so (declared in include/pntf.h): argument checks, launch geometry,
 // error reporting.  Device code lives in pntf_field.hip.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "pntf.h"
@@ -22,7 +23,7 @@ template <int DIM>
 __global__ void plan_split_kernel(PlanArgs a);
 template <int DIM, int KIND>
 __global__ void field_quad_kernel(FieldArgs a);
-template <int DIM>
+template <int DIM, bool SOLO>
 __global__ void plan_quad_kernel(PlanArgs a);
 template <int DIM>
 __global__ void residual_kernel(ResidualArgs a);
@@ -100,6 +101,16 @@ static int64_t quad_grid_for(int64_t n) {
 
 // Quad tiles while every tile gets a CU of its own: a planner step of a 4-pair tile is bound
 // by the CU's weight stream, not by its MFMAs.
+// PNTF_QSOLO=0 in the environment (read once) runs single-query plans on the MFMA quad
+// layers instead of the VALU SOLO layers (to compare the two).
+static bool solo_enabled() {
+  static const int on = [] {
+    const char* e = getenv("PNTF_QSOLO");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 static bool use_quad(int64_t n, int schedule) {
   if (schedule == PNTF_SCHED_QUAD_TILE) return true;
   if (schedule != PNTF_SCHED_AUTO) return false;
@@ -401,8 +412,13 @@ int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, cons
              (float*)ws};
   if (use_quad(q, schedule)) {   // no workspace
     dim3 g((unsigned)quad_grid_for(q)), b(256);
-    if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3>), g, b, 0, stream, a);
-    else hipLaunchKernelGGL((plan_quad_kernel<6>), g, b, 0, stream, a);
+    if (q == 1 && solo_enabled()) {   // the reference's Q = 1 loop: VALU layers, one pair
+      if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3, true>), g, b, 0, stream, a);
+      else hipLaunchKernelGGL((plan_quad_kernel<6, true>), g, b, 0, stream, a);
+      return check_launch("plan_quad_kernel<solo>");
+    }
+    if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3, false>), g, b, 0, stream, a);
+    else hipLaunchKernelGGL((plan_quad_kernel<6, false>), g, b, 0, stream, a);
     return check_launch("plan_quad_kernel");
   }
   if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");

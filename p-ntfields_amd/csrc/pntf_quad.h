@@ -97,6 +97,7 @@ __device__ __forceinline__ float pick(const f32x4& v, int g) {
 struct QCx {
   lds_f* lds;
   int w, lane, og, kb, l16;
+  int sp;   // the pair a SOLO layer reads (0: the single query)
   __device__ lds_f* buf(int b) const { return lds + b * QBUF; }
   __device__ lds_f* sig(int slot) const { return lds + 3 * QBUF + (w * QNSIG + slot) * 64 + lane; }
   __device__ lds_f* red(int wave, int v) const { return lds + Q_RED + (wave * 12 + v) * 4; }
@@ -128,14 +129,15 @@ __device__ __forceinline__ void qfetch(QRing<QR>& ring, Rsrc W, int lane, int sl
 // One layer: G groups of 16 out rows; per group IN/16 fragments of 4 k steps x NC columns;
 // B operands read from `in` (IN features, row stride IN/4 + 4).  The layer's first fragment
 // sits in ring slot S0.  epi(g, v[NC]) gets the compact sums of group g.
-template <int NC, int IN, int NF, int G, int S0, int QR, class Epi>
+template <int NC, int IN, int NF, int G, int S0, int QR, bool SOLO, class Epi>
 __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, const lds_f* in,
                                        Epi&& epi) {
   constexpr int SP = IN / 4 + 4, NQ = IN / 16;
   // B operands kept in registers for all groups of the layer when they fit (64 VGPRs):
   // one LDS read per fragment instead of one per fragment and group
   constexpr bool KEEP = PNTF_QKEEPB && G > 1 && NC * NQ <= 16;
-  const lds_f* src = in + cx.l16 * SP;
+  // SOLO: every lane reads the one active pair's B operands (row kb, pair cx.sp)
+  const lds_f* src = in + (SOLO ? ((cx.l16 & ~3) | cx.sp) : cx.l16) * SP;
   f32x4 xb[KEEP ? NC : 1][KEEP ? NQ : 1];
   if constexpr (KEEP) {
 #pragma unroll
@@ -143,6 +145,49 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
         xb[c][q] = *reinterpret_cast<const lds_f4*>(src + c * 16 * SP + 4 * q);
+  }
+  if constexpr (SOLO) {
+  // one active query in the tile (planner): the fragment runs on the VALU for that pair
+  // (4 FMAs per column instead of 4 MFMAs of which 3 columns are idle); each lane's sum is
+  // row r0 + 4·og + (l & 3) over its k sub-block kb, and every pair slot carries the values
+  static_for<0, G>([&](auto gg) {
+    constexpr int g = decltype(gg)::value;
+    const lds_f* src0 = src;
+    float acc[NC][QCH];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int h = 0; h < QCH; ++h) acc[c][h] = 0.f;
+    static_for<0, NQ>([&](auto qq) {
+      constexpr int q = decltype(qq)::value, slot = (S0 + g * NQ + q) % QR;
+      f32x4 b[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if constexpr (KEEP) b[c] = xb[c][q];
+        else b[c] = *reinterpret_cast<const lds_f4*>(src0 + c * 16 * SP + 4 * q);
+      }
+      const f32x4 a = ring.r[slot];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c][e % QCH] = fmaf(a[e], b[c][e], acc[c][e % QCH]);
+      qfetch<NF, QR>(ring, W, cx.lane, slot);
+    });
+    float v[NC];
+    // the compact value of lane l is row r0 + 4·og + kb (the MFMA path's layout): take it
+    // from the lane of the same og whose (l & 3) is this lane's kb
+    const int src_lane = (cx.lane & 0x30) | cx.kb;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float t = acc[c][0];
+#pragma unroll
+      for (int h = 1; h < QCH; ++h) t += acc[c][h];
+      t = dpp_add<0x128>(dpp_add<0x124>(t));
+      v[c] = __shfl(t, src_lane);
+    }
+    epi(g, v);
+  });
+  return;
   }
   static_for<0, G>([&](auto gg) {
     constexpr int g = decltype(gg)::value;
@@ -209,7 +254,7 @@ __device__ __forceinline__ void qreduce(const QCx& cx, float (&v)[NV]) {
 
 // Forward pass (NN.out, :215-259) for the 4 pairs of the tile; returns τ of the lane's pair.
 // GRAD: save σ10 for the reverse sweep.  Buffers: 0 = features / dz, 1 = A, 2 = B.
-template <int DIM, bool GRAD, int NF, int QR>
+template <int DIM, bool GRAD, int NF, int QR, bool SOLO = false>
 __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx& cx,
                                               const PairIO& io, const f32x4 (&aux)[Q_NAUX],
                                               int compat) {
@@ -238,7 +283,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[0] (:227); compat: the out_backgrad quirk (:435-438) stores σ10(softplus(y))
-  qlayer<2, 256, NF, 2, 0 % QR, QR>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
+  qlayer<2, 256, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       SpSig q = sp_sig(v[c] + pick(aux[0], g));
@@ -251,7 +296,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int la = 1 + 2 * blk, sa = QS_EBLK + 8 * blk;
-    qlayer<2, 128, NF, 2, 0 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         SpSig q = sp_sig(v[c] + pick(aux[la], g));
@@ -260,7 +305,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
       }
     });
     qsync();
-    qlayer<2, 128, NF, 2, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -272,7 +317,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
     qsync();
   }
   // ---- encoder[-1] (:234) and the smooth max / min merge (:236-244): u = [M | m] -> B
-  qlayer<2, 128, NF, 2, 0 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const float zs = v[0] + pick(aux[5], g), zg = v[1] + pick(aux[5], g);
     const float d = zs - zg;
     const float e = exp_neg10abs(d);
@@ -291,13 +336,13 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   for (int i = 0; i < 3; ++i) {
     const f32x4 ba = i == 0 ? aux[6] : i == 1 ? aux[8] : aux[10];
     const f32x4 bb = i == 0 ? aux[7] : i == 1 ? aux[9] : aux[11];
-    qlayer<1, 256, NF, 4, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       SpSig q = sp_sig(v[0] + pick(ba, g));
       *cx.at<256>(A, 0, g) = q.sp;
       if (GRAD) *cx.sig(QS_GBLK + 8 * i + g) = q.sg;
     });
     qsync();
-    qlayer<1, 256, NF, 4, 16 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       SpSig q = sp_sig(v[0] + pick(bb, g) + *o);
       *o = q.sp;
@@ -307,7 +352,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   // ---- generator[-2] + act (:251-252) and the head generator[-1] (:254-255)
   float part[1] = {0.f};
-  qlayer<1, 256, NF, 2, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+  qlayer<1, 256, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
     SpSig q = sp_sig(v[0] + pick(aux[12], g));
     part[0] = fmaf(pick(aux[13], g), q.sp, part[0]);
     if (GRAD) *cx.sig(QS_G3 + g) = q.sg;
@@ -319,7 +364,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
 
 // Reverse sweep (exact, or out_backgrad when the forward stored the quirk): dτ/dxs, dτ/dxg of
 // the lane's pair, identical in all lanes of the pair.
-template <int DIM, int NF, int QR>
+template <int DIM, int NF, int QR, bool SOLO = false>
 __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx& cx,
                                               const PairIO& io, float tau,
                                               const f32x4 (&aux)[Q_NAUX], float (&ds)[DIM],
@@ -331,19 +376,19 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   for (int g = 0; g < 2; ++g) *cx.at<128>(A, 0, g) = dd * pick(aux[13], g) * *cx.sig(QS_G3 + g);
   qsync();
   // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> B
-  qlayer<1, 128, NF, 4, 16 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+  qlayer<1, 128, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
     *cx.at<256>(B, 0, g) = v[0] * *cx.sig(QS_GBLK + 16 + 4 + g);
   });
   qsync();
   // ---- generator blocks, reverse (:615-618): lb: B -> A, la: A (+ B residual) -> B
 #pragma unroll 1
   for (int i = 2; i >= 0; --i) {
-    qlayer<1, 256, NF, 4, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * i + g);
     });
     qsync();
     const int sb = QS_GBLK + 8 * (i - 1) + 4;   // σ10(y2) of block i - 1 (none for i = 0)
-    qlayer<1, 256, NF, 4, 16 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       const float y = v[0] + *o;
       *o = i > 0 ? y * *cx.sig(sb + g) : y;
@@ -361,7 +406,7 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1): F -> A
-  qlayer<2, 128, NF, 2, 16 % QR, QR>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) *cx.at<128>(A, c, g) = v[c] * *cx.sig(QS_EBLK + 12 + 2 * g + c);
   });
@@ -371,12 +416,12 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
 #pragma unroll
   for (int blk = 1; blk >= 0; --blk) {
     const int sa = QS_EBLK + 8 * blk, sbelow = blk ? QS_EBLK + 4 : QS_E0;
-    qlayer<2, 128, NF, 2, 0 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) *cx.at<128>(B, c, g) = v[c] * *cx.sig(sa + 2 * g + c);
     });
     qsync();
-    qlayer<2, 128, NF, 2, 16 % QR, QR>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -390,7 +435,7 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   float acc[2 * DIM];
 #pragma unroll
   for (int i = 0; i < 2 * DIM; ++i) acc[i] = 0.f;
-  qlayer<2, 128, NF, 4, 0 % QR, QR>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 4, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const int f = cx.w * 64 + 16 * g + 4 * cx.og + cx.kb;
     const int fb = f & 127;
     float bw[DIM];
@@ -438,6 +483,7 @@ __device__ __forceinline__ QCx quad_cx(lds_f* lds) {
   cx.og = cx.lane >> 4;
   cx.kb = (cx.lane >> 2) & 3;
   cx.l16 = cx.lane & 15;
+  cx.sp = 0;
   return cx;
 }
 
@@ -477,7 +523,10 @@ __global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
 
 // Batched planner on quad tiles: one workgroup per 4-query tile (grid-stride), the loop of
 // plan_kernel (test/gib_plan.py:74-86, test/arm_plan.py:140-152) with per-query freeze.
-template <int DIM>
+// SOLO (a single query: the reference's Q = 1 loop, q == 1): the layers run as VALU dot
+// products for pair 0 (qlayer), its values copied into the three other pair slots (whose
+// inputs are never read and whose outputs are never stored).
+template <int DIM, bool SOLO>
 __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
   __shared__ float smem[Q_LDS_FLOATS];
   const QCx cx = quad_cx((lds_f*)smem);
@@ -522,9 +571,10 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
     int it = 0;
     for (; it < cap; ++it) {
       if (!__any(active)) break;
-      const float tau = quad_forward<DIM, true, Q_NF_ALL, QRING>(ring, W, cx, io, aux, a.compat);
+      const float tau =
+          quad_forward<DIM, true, Q_NF_ALL, QRING, SOLO>(ring, W, cx, io, aux, a.compat);
       float ds[DIM], dg[DIM], vs[DIM], vg[DIM];
-      quad_backward<DIM, Q_NF_ALL, QRING>(ring, W, cx, io, tau, aux, ds, dg);
+      quad_backward<DIM, Q_NF_ALL, QRING, SOLO>(ring, W, cx, io, tau, aux, ds, dg);
       path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
       if (active) {
 #pragma unroll

@@ -88,8 +88,11 @@ UNITS = (
     + [("quad_d%d_k%d" % (d, k), "pntf_kernels.hip",
         ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_QUAD_FIELD"])
        for d in (3, 6) for k in range(5)]
-    + [("plan_quad_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD"])
-       for d in (3, 6)]
+    + [("plan_quad_d%d" % d, "pntf_kernels.hip",
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=0"]) for d in (3, 6)]
+    # single-query planner (the reference's Q = 1 loop): quad layout, layers on the VALU
+    + [("plan_quad_solo_d%d" % d, "pntf_kernels.hip",
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=1"]) for d in (3, 6)]
     + [("residual_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_RESIDUAL"])
        for d in (3, 6)]
     + [("util", "pntf_kernels.hip", ["-DPNTF_UTIL"]), ("capi", "pntf_capi.hip", []),
@@ -176,7 +179,7 @@ def _compile(unit, uid=None):
     # A VGPR "spill" with no scratch is a copy into an AGPR (a register move); spills to
     # scratch memory are what broke the 2-waves/SIMD build, and those fail the build.
     bad = {k: v for k, v in res.items() if v.get("ScratchSize [bytes/lane]", 0) or (
-        v.get("VGPRs Spill", 0) and not name.startswith("wide_"))}
+        v.get("VGPRs Spill", 0) and not name.startswith(("wide_", "plan_quad_")))}
     if bad:
         raise RuntimeError("VGPR spills / scratch in %s: %s" % (name, bad))
     if SGPR_SPILL_FREE.match(name):

@@ -377,3 +377,19 @@ def test_planner_edge_cases(packed, dev, schedule, W):
                             max_iter=max_iter, compat=True)
             assert steps[i] == so[0] == max_iter + 1
             assert np.abs(path[i] - po[0]).max() < 1e-5
+
+
+@pytest.mark.parametrize("golden", ["plan_gib.npz", "plan_arm.npz"])
+def test_single_query_planner_vs_reference(packed, dev, golden):
+    """The reference plans one query at a time (test/gib_plan.py, test/arm_plan.py: Q = 1).
+    A single-query call runs plan_quad_solo_kernel (VALU layers for the one pair): every
+    golden query planned alone gives the reference's iteration count and path within 1e-3."""
+    p = load(golden)
+    gib = golden == "plan_gib.npz"
+    B = T(p["B"] if gib else p["B"].T, dev)
+    kw = (dict(dim=3, step=0.03, tol=0.06, max_iter=500, mode=ops.GRAD_BACKGRAD_COMPAT) if gib
+          else dict(dim=6, step=0.015, tol=0.03, max_iter=300, mode=ops.GRAD_EXACT))
+    for i in range(len(p["iters"])):
+        path, steps = ops.plan(packed, T(p["starts"][i:i + 1], dev), B, **kw)
+        assert int(steps.cpu()[0]) == int(p["iters"][i]), i
+        assert np.abs(path.cpu().numpy()[0] - p["paths"][i]).max() < 1e-3, i

@@ -264,3 +264,22 @@ def test_w2_c5_1024_queries_vs_reference(arm):
         float(np.quantile(err, 0.99)), float(err.max()), int((err > 1e-3).sum()))
     s16 = same[:16]
     assert np.abs(path[:16][s16] - c["paths16"][s16]).max() < 1e-3
+
+
+@pytest.mark.gpu
+def test_w2_single_query_planners_vs_reference(multi, arm):
+    """Trained weights, one query per call (the reference's Q = 1 loop, 100-230-step plans)
+    on plan_quad_solo_kernel: iteration counts identical, paths within 1e-3."""
+    from pntf import ops
+    dev = torch.device("cuda:0")
+    for net, name, B, kw in (
+            (multi, "plan_gib_w2.npz", lambda f: f["B"],
+             dict(dim=3, step=0.03, tol=0.06, max_iter=500, mode=ops.GRAD_BACKGRAD_COMPAT)),
+            (arm, "plan_arm_w2.npz", lambda f: f["B"].T,
+             dict(dim=6, step=0.015, tol=0.03, max_iter=300, mode=ops.GRAD_EXACT))):
+        f = load(name)
+        for i in range(len(f["iters"])):
+            path, steps = ops.plan(net.network.packed(), _T(f["starts"][i:i + 1], dev),
+                                   _T(B(f), dev), **kw)
+            assert int(steps.cpu()[0]) == int(f["iters"][i]), (name, i)
+            assert np.abs(path.cpu().numpy()[0] - f["paths"][i]).max() < 1e-3, (name, i)

@@ -77,6 +77,18 @@ def main():
         json.dump(j, fh, indent=1)
     shutil.copy(p, os.path.join(PROF, "pmc_tau_grad.json"))
     print(json.dumps(j, indent=1))
+    if os.path.exists(os.path.join(OUT, "pmc_stall", "run_counter_collection.csv")):
+        st, ns = counters("pmc_stall", a.kernel)
+        k = {"kernel": a.kernel, "unit": a.unit, "unit_hash": unit_hash,
+             "dispatches": ns.get("SQ_WAIT_ANY"), **{c: st[c] for c in sorted(st)},
+             "wait_any_frac_of_wave_cycles": st["SQ_WAIT_ANY"] / st["SQ_WAVE_CYCLES"],
+             "wait_inst_any_frac_of_wave_cycles": st["SQ_WAIT_INST_ANY"] / st["SQ_WAVE_CYCLES"],
+             "notes": "SQ_WAIT_ANY: wave parked on s_waitcnt (memory); SQ_WAIT_INST_ANY also "
+                      "counts waits for the MFMA pipe, which an MFMA-bound kernel spends most "
+                      "cycles in."}
+        with open(os.path.join(PROF, "%s_pmc_stall_tau_grad.json" % a.tag), "w") as fh:
+            json.dump(k, fh, indent=1)
+        print("stall: SQ_WAIT_ANY %.4f of wave-cycles" % k["wait_any_frac_of_wave_cycles"])
 
 
 if __name__ == "__main__":

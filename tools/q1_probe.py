@@ -1,0 +1,33 @@
+"""Batch-1 planner step time (test/gib_plan.py runs Q = 1) and the C5 plan, as bench.py's
+extras measure them; run once with PNTF_QSOLO=0 to time the MFMA quad kernel instead of the
+single-query VALU kernel."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "p-ntfields_amd"))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from pntf import ops, synth  # noqa: E402
+
+if __name__ == "__main__":
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    W = synth.make_weights(0)
+    packed = ops.pack_weights([torch.from_numpy(v).to(dev) for v in W.values()])
+    out = {"solo": os.environ.get("PNTF_QSOLO", "1")}
+    for dim, B, kw in ((3, synth.make_B(3, seed=1), dict(step=0.03, mode=ops.GRAD_BACKGRAD_COMPAT)),
+                       (6, synth.make_B(6, seed=12, arm=True).T.copy(),
+                        dict(step=0.015, mode=ops.GRAD_EXACT))):
+        x1 = torch.from_numpy(synth.make_pairs(1, dim, seed=21)).to(dev)
+        Bt = torch.from_numpy(B).to(dev)
+        res = {}
+
+        def run1():
+            res["p"] = ops.plan(packed, x1, Bt, dim=dim, tol=1e-9, max_iter=99, **kw)
+        out["q1_ms_per_step_d%d" % dim] = bench._timeit(run1, reps=5) / 100.0
+    print(json.dumps(out), flush=True)

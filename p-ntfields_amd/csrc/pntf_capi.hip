@@ -101,8 +101,8 @@ static int64_t quad_grid_for(int64_t n) {
 
 // Quad tiles while every tile gets a CU of its own: a planner step of a 4-pair tile is bound
 // by the CU's weight stream, not by its MFMAs.
-// PNTF_QSOLO=0 in the environment (read once) runs single-query plans on the MFMA quad
-// layers instead of the VALU SOLO layers (to compare the two).
+// PNTF_QSOLO=0 in the environment (read once) runs batches of at most one query per CU on
+// the MFMA quad layers instead of the VALU SOLO layers (to compare the two).
 static bool solo_enabled() {
   static const int on = [] {
     const char* e = getenv("PNTF_QSOLO");
@@ -412,9 +412,11 @@ int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, cons
              (float*)ws};
   if (use_quad(q, schedule)) {   // no workspace
     dim3 g((unsigned)quad_grid_for(q)), b(256);
-    if (q == 1 && solo_enabled()) {   // the reference's Q = 1 loop: VALU layers, one pair
-      if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3, true>), g, b, 0, stream, a);
-      else hipLaunchKernelGGL((plan_quad_kernel<6, true>), g, b, 0, stream, a);
+    if (q <= (int64_t)num_cus() && solo_enabled()) {
+      // one query per CU (the reference's Q = 1 loop, small batches): VALU SOLO layers
+      dim3 gs((unsigned)q);
+      if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3, true>), gs, b, 0, stream, a);
+      else hipLaunchKernelGGL((plan_quad_kernel<6, true>), gs, b, 0, stream, a);
       return check_launch("plan_quad_kernel<solo>");
     }
     if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3, false>), g, b, 0, stream, a);

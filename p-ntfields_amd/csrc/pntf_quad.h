@@ -523,9 +523,10 @@ __global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
 
 // Batched planner on quad tiles: one workgroup per 4-query tile (grid-stride), the loop of
 // plan_kernel (test/gib_plan.py:74-86, test/arm_plan.py:140-152) with per-query freeze.
-// SOLO (a single query: the reference's Q = 1 loop, q == 1): the layers run as VALU dot
-// products for pair 0 (qlayer), its values copied into the three other pair slots (whose
-// inputs are never read and whose outputs are never stored).
+// SOLO (one query per workgroup: the reference's Q = 1 loop, and any batch of at most one
+// query per CU): the tile is a single query, loaded into all four pair slots; the layers run
+// as VALU dot products for pair slot 0 (qlayer), the other slots carry the same values, and
+// only slot 0 stores.
 template <int DIM, bool SOLO>
 __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
   __shared__ float smem[Q_LDS_FLOATS];
@@ -542,14 +543,15 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
   for (int s = 0; s < QRING; ++s) qfetch<Q_NF_ALL, QRING>(ring, W, cx.lane, s);
   const int cap = a.max_iter + 1;
   const int64_t rows = (int64_t)cap + 1;
-  const int64_t ntiles = (a.q + QPAIRS - 1) / QPAIRS;
+  constexpr int TQ = SOLO ? 1 : QPAIRS;   // queries per tile
+  const int64_t ntiles = (a.q + TQ - 1) / TQ;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t qi = tile * QPAIRS + (cx.lane & 3);
+    const int64_t qi = SOLO ? tile : tile * QPAIRS + (cx.lane & 3);
     PairIO io;
     const bool ok = load_pair<DIM>(a.xp0, a.Btab, a.env, a.q, a.n_env, qi, io);
     quad_stage_b<DIM>(cx, io);
     qsync();
-    const bool store = cx.w == 0 && cx.lane < QPAIRS && qi < a.q;
+    const bool store = cx.w == 0 && cx.lane < TQ && qi < a.q;
     float* prow = a.path + (store ? qi : 0) * rows * 2 * DIM;
     auto dist = [&]() {
       float s = 0.f;

@@ -1,6 +1,6 @@
-"""Batch-1 planner step time (test/gib_plan.py runs Q = 1) and the C5 plan, as bench.py's
-extras measure them; run once with PNTF_QSOLO=0 to time the MFMA quad kernel instead of the
-single-query VALU kernel."""
+"""Planner step time at Q = 1 (test/gib_plan.py's batch), 16 and 256 queries, as bench.py's
+extras measure it; run once with PNTF_QSOLO=0 to time the MFMA quad layers instead of the
+one-query-per-CU SOLO layers."""
 import json
 import os
 import sys
@@ -30,4 +30,10 @@ if __name__ == "__main__":
         def run1():
             res["p"] = ops.plan(packed, x1, Bt, dim=dim, tol=1e-9, max_iter=99, **kw)
         out["q1_ms_per_step_d%d" % dim] = bench._timeit(run1, reps=5) / 100.0
+        for q in (16, 256):
+            xq = torch.from_numpy(synth.make_pairs(q, dim, seed=22)).to(dev)
+
+            def runq():
+                res["p"] = ops.plan(packed, xq, Bt, dim=dim, tol=1e-9, max_iter=99, **kw)
+            out["q%d_ms_per_step_d%d" % (q, dim)] = bench._timeit(runq, reps=5) / 100.0
     print(json.dumps(out), flush=True)

@@ -438,3 +438,36 @@ def test_fused_linear_act_matches_two_pass(dim, n):
     assert _rel(d1, d2) < 1e-5
     for k in g1:
         assert _rel(g1[k], g2[k]) < 1e-5, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["misaligned", "beta_half", "narrow_k"])
+def test_panel_gemm_fallbacks_vs_fp64(case):
+    """Shapes / operands the register-panel kernel does not take fall back to the LDS-tiled
+    kernel and stay exact: a 4-byte-misaligned A (torch view at an odd float offset), beta
+    other than 0 / 1, and K outside {128, 256}.  The panel path itself is covered by
+    test_mfma_gemm_vs_fp64 (forward / input-gradient shapes) and the training tests."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(7)
+    M, N, K, beta = 3001, 256, 256, 0.0
+    if case == "beta_half":
+        beta = 0.5
+    if case == "narrow_k":
+        K = 64
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    if case == "misaligned":
+        buf = torch.empty(M * K + 1, device=dev)
+        Ad = buf[1:].view(M, K)
+        Ad.copy_(A.to(dev))
+        assert Ad.data_ptr() % 16 != 0
+    else:
+        Ad = A.to(dev)
+    C = C0.to(dev)
+    train.gemm(C, Ad, B.to(dev), False, True, beta)
+    ref = A.double() @ B.double().t() + beta * C0.double()
+    scale = A.double().abs() @ B.double().abs().t()
+    err = (C.cpu().double() - ref).abs()
+    assert torch.all(err <= 1e-5 * np.sqrt(K) * scale + 1e-6), float((err / scale).max())

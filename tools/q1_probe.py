@@ -36,4 +36,14 @@ if __name__ == "__main__":
             def runq():
                 res["p"] = ops.plan(packed, xq, Bt, dim=dim, tol=1e-9, max_iter=99, **kw)
             out["q%d_ms_per_step_d%d" % (q, dim)] = bench._timeit(runq, reps=5) / 100.0
+    # C5: 1024 arm queries, <= 199 steps, per-query freeze (bench.py's extra)
+    Ba = torch.from_numpy(synth.make_B(6, seed=12, arm=True).T.copy()).to(dev)
+    xq = torch.from_numpy(synth.make_box_pairs(1024, 6, seed=3)).to(dev)
+    res = {}
+
+    def c5():
+        res["p"] = ops.plan(packed, xq, Ba, dim=6, step=0.015, tol=0.03, max_iter=199,
+                            mode=ops.GRAD_EXACT)
+    out["c5_ms"] = bench._timeit(c5, reps=5)
+    out["c5_max_steps"] = int(res["p"][1].max())
     print(json.dumps(out), flush=True)

@@ -59,8 +59,11 @@ def parse(argv=None):
     ap.add_argument("--envs", type=int, default=10)
     ap.add_argument("--mode", choices=["exact", "compat"], default="exact")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--force-gather", action="store_true",
+                    help="build the RCCL group and run the all-gather even at N = 1 (a "
+                         "one-rank collective: measures the exchange path on one GPU)")
     ap.add_argument("--roofline-launches", type=int, default=100)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_tau_grad.json"))
@@ -82,29 +85,42 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(seconds, n_chunk=4096):
+def cpu_baseline(sizes=(4096, 262144), reps=5):
     """The reference's CPU op sequence (torch Linear/Softplus/logsumexp + autograd.grad with
-    create_graph, oracle/torch_ref.py) on a bounded sample of the same workload."""
+    create_graph, oracle/torch_ref.py, pinned to the reference by
+    tests/test_oracle_golden.py::test_torch_ref_cpu_baseline_vs_reference) on the same
+    synthetic workload, as SURVEY.md §8(d) specifies: all host threads
+    (torch.set_num_threads), one warm-up call, then the median of `reps` timed calls at each
+    batch size.  `value` is the rate at the largest size."""
     from oracle.torch_ref import TorchRef
     from pntf import synth
     threads = int(os.environ.get("OMP_NUM_THREADS", 0) or os.cpu_count() or 1)
     torch.set_num_threads(threads)
     ref = TorchRef(synth.make_weights(0))
-    xp = synth.make_pairs(n_chunk, 3, seed=2)
     Bt = synth.make_B_table(10, 3)
-    env = synth.make_env_ids(n_chunk, 10)
-    ref.tau_grad(xp[:256], Bt, env[:256])                          # warm-up
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        ref.tau_grad(xp, Bt, env)
-        done += n_chunk
-    el = time.perf_counter() - t0
-    return {"value": done / el, "unit": UNIT, "cores": torch.get_num_threads(),
-            "kind": "port", "cpu_model": cpu_model(),
-            "sample": "%d pairs (%d-pair batches, 10 envs, per-pair env id) of the same "
-                      "synthetic workload through oracle/torch_ref.py (the reference's torch "
-                      "CPU op sequence: NN.out + Model.gradient autograd, create_graph=True), "
-                      "fp32, %.1f s" % (done, n_chunk, el)}
+    per_size, total = {}, 0.0
+    for n in sizes:
+        xp = synth.make_pairs(n, 3, seed=2)
+        env = synth.make_env_ids(n, 10)
+        ref.tau_grad(xp, Bt, env)                                     # warm-up
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ref.tau_grad(xp, Bt, env)
+            ts.append(time.perf_counter() - t0)
+        total += sum(ts)
+        med = float(np.median(ts))
+        per_size[str(n)] = {"pairs_per_s": n / med, "median_s": med,
+                            "min_s": float(min(ts)), "max_s": float(max(ts)), "reps": reps}
+    big = str(max(sizes))
+    return {"value": per_size[big]["pairs_per_s"], "unit": UNIT,
+            "cores": torch.get_num_threads(), "kind": "port", "cpu_model": cpu_model(),
+            "sizes": per_size,
+            "sample": "median of %d reps after one warm-up at N = %s pairs (10 envs, per-pair "
+                      "env id; `value` at N = %s) of the same synthetic workload through "
+                      "oracle/torch_ref.py (the reference's torch CPU op sequence: NN.out + "
+                      "Model.gradient autograd, create_graph=True), fp32, %.1f s timed"
+                      % (reps, " and ".join(str(s) for s in sizes), big, total)}
 
 
 def pmc_traffic(path, pairs, unit_hash):
@@ -197,7 +213,7 @@ def run(args):
     rank, ws, local = dist.world()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist.init("nccl", device=dev)
+    dist.init("nccl", device=dev, force=args.force_gather)
     if ws > 1 and tdist.get_world_size() != args.gpus:
         raise RuntimeError("RCCL world size %d != --gpus %d" % (tdist.get_world_size(),
                                                                   args.gpus))
@@ -211,16 +227,19 @@ def run(args):
     Bt = torch.from_numpy(synth.make_B_table(args.envs, 3)).to(dev)
     env_all = synth.make_env_ids(n_total, args.envs)
     env = torch.from_numpy(env_all[lo:lo + n].copy()).to(dev)
-    gather = ws > 1 and not args.no_gather
+    gather = (ws > 1 or args.force_gather) and not args.no_gather
     res = {}
 
     def kernel():
         return ops.tau_grad(packed, xp, Bt, env, dim=3, mode=mode)
 
+    def rows(t, d):
+        return torch.cat([t.unsqueeze(1), d], 1)
+
     def step():
         t, d = kernel()
         if gather:
-            res["g"] = dist.all_gather_rows(torch.cat([t.unsqueeze(1), d], 1), n_total)
+            res["g"] = dist.all_gather_rows(rows(t, d), n_total, force=args.force_gather)
 
     el = timed(step, args.steps, args.warmup, ws, torch.cuda.synchronize, dev)
     value = n_total * args.steps / el
@@ -241,6 +260,29 @@ def run(args):
     achieved = FLOP_PER_PAIR * n / (kern_ms * 1e-3) / 1e12
     unit_hash = _lib.build_info().get(HEADLINE_UNIT)
     traffic, traffic_src = pmc_traffic(args.pmc, n, unit_hash)
+    split = None
+    if gather:
+        # the exchange alone (same row block, same stream), so a scaling run separates
+        # per-rank compute from the xGMI all-gather; every rank's numbers go to rank 0
+        blk = rows(*kernel())
+        dist.all_gather_rows(blk, n_total, force=args.force_gather)
+        torch.cuda.synchronize()
+        gevs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(R)]
+        for a, b in gevs:
+            a.record(stream)
+            dist.all_gather_rows(blk, n_total, force=args.force_gather)
+            b.record(stream)
+        torch.cuda.synchronize()
+        ag_ms = float(np.mean([a.elapsed_time(b) for a, b in gevs]))
+        mine = torch.tensor([kern_ms, ag_ms], dtype=torch.float64, device=dev)
+        every = [torch.zeros_like(mine) for _ in range(tdist.get_world_size())]
+        tdist.all_gather(every, mine)
+        every = torch.stack(every).cpu().numpy()
+        split = {"kernel_ms_per_rank": every[:, 0].tolist(),
+                 "allgather_ms_per_rank": every[:, 1].tolist(),
+                 "allgather_bytes_per_rank": int(blk.numel() * blk.element_size()),
+                 "rccl_world_size": tdist.get_world_size()}
 
     extra = {}
     if not args.no_extra:
@@ -250,7 +292,7 @@ def run(args):
             extra = sharded_extras(packed, dev, rank, ws)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_seconds)          # last: after every GPU leg
+        cpu = cpu_baseline(reps=args.cpu_reps)        # last: after every GPU leg
 
     if rank == 0:
         line = {
@@ -263,7 +305,8 @@ def run(args):
                        "pairs_per_gpu": n, "global_batch": n_total, "envs": args.envs,
                        "grad_mode": args.mode, "allgather_outputs": gather,
                        "parallelism": "dp%d" % ws,
-                       "rccl_world_size": tdist.get_world_size() if ws > 1 else 1},
+                       "rccl_world_size": tdist.get_world_size() if tdist.is_initialized()
+                       else 1},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,
@@ -274,10 +317,12 @@ def run(args):
                          "algorithmic_bytes_per_pair": BYTES_PER_PAIR},
             "cpu_baseline": cpu,
         }
+        if split:
+            line["exchange"] = split
         if extra:
             line["extra"] = extra
         print(json.dumps(line), flush=True)
-    if ws > 1:
+    if tdist.is_initialized():
         tdist.barrier()
         tdist.destroy_process_group()
     return 0
@@ -298,7 +343,8 @@ def _timeit(fn, reps=5):
 
 def sharded_extras(packed, dev, rank, ws, q=1024):
     """N > 1: the C5 arm planner with its 1024 queries sharded over the ranks, then the RCCL
-    all-gather of every rank's paths (the planner-path exchange of SURVEY.md §8e)."""
+    all-gather of every rank's paths (the planner-path exchange of SURVEY.md §8e); the wall
+    time of both, and per rank the planner kernel alone and the all-gather alone."""
     from pntf import ops, synth
     Ba = torch.from_numpy(synth.make_B(6, seed=12, arm=True).T.copy()).to(dev)
     xq_all = synth.make_box_pairs(q, 6, seed=3)
@@ -306,14 +352,28 @@ def sharded_extras(packed, dev, rank, ws, q=1024):
     xq = torch.from_numpy(xq_all[lo:hi].copy()).to(dev)
     res = {}
 
-    def run():
-        path, steps = ops.plan(packed, xq, Ba, dim=6, step=0.015, tol=0.03, max_iter=199,
-                               mode=ops.GRAD_EXACT)
+    def plan():
+        res["local"] = ops.plan(packed, xq, Ba, dim=6, step=0.015, tol=0.03, max_iter=199,
+                                mode=ops.GRAD_EXACT)
+
+    def gather():
+        path, steps = res["local"]
         res["paths"] = dist.all_gather_rows(path, q)
         res["steps"] = dist.all_gather_rows(steps, q)
 
+    def run():
+        plan()
+        gather()
+
     el = timed(run, 3, 1, ws, torch.cuda.synchronize, dev)
+    mine = torch.tensor([_timeit(plan, reps=3), _timeit(gather, reps=3)], dtype=torch.float64,
+                        device=dev)
+    every = [torch.zeros_like(mine) for _ in range(ws)]
+    tdist.all_gather(every, mine)
+    every = torch.stack(every).cpu().numpy()
     return {"c5_arm_plan_1024q_sharded_allgather_ms": el / 3 * 1e3,
+            "c5_plan_kernel_ms_per_rank": every[:, 0].tolist(),
+            "c5_path_allgather_ms_per_rank": every[:, 1].tolist(),
             "c5_arm_plan_mean_steps": float(res["steps"].float().mean().item())}
 
 

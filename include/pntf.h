@@ -87,6 +87,13 @@ int pntf_set_field_schedule(int schedule);
  * Profiles under profiles/ record the hash of the unit they measured. */
 const char* pntf_build_info(void);
 
+/* The kernel family (PNTF_SCHED_QUAD/SPLIT/WIDE/WAVE_TILE) a field entry point runs for n
+ * pairs when asked for `schedule`; -1 for a negative n or an unknown schedule.  Host-only
+ * (no device work; the CU count comes from the current device, 256 without one).  Batches of
+ * more than 2^31 - 32 pairs never run WIDE_TILE (its 32-bit tile index): they fall back to
+ * WAVE_TILE. */
+int pntf_field_schedule_for(int64_t n, int schedule);
+
 /* Device scratch needed by the gradient/planner entry points for n pairs. */
 size_t pntf_workspace_bytes(int64_t n);
 

@@ -145,6 +145,19 @@ static bool valid_schedule(int s) {
          s == PNTF_SCHED_WIDE_TILE || s == PNTF_SCHED_QUAD_TILE;
 }
 
+// wide_field_kernel keeps its tile index in a 32-bit SGPR (pntf_wide.h): the first pair of the
+// last tile, tile * WTILE, must stay below 2^31.  Larger batches run the wave-tile kernel
+// (int64 tile index) whatever schedule was asked for.
+static constexpr int64_t WIDE_MAX_PAIRS = (int64_t)0x7fffffff - WTILE + 1;
+
+// The kernel family a field call of n pairs runs (PNTF_SCHED_QUAD/SPLIT/WIDE/WAVE_TILE).
+static int resolve_field_schedule(int64_t n, int schedule) {
+  if (use_quad(n, schedule)) return PNTF_SCHED_QUAD_TILE;
+  if (use_split(n, schedule)) return PNTF_SCHED_SPLIT_TILE;
+  if (schedule == PNTF_SCHED_WAVE_TILE || n > WIDE_MAX_PAIRS) return PNTF_SCHED_WAVE_TILE;
+  return PNTF_SCHED_WIDE_TILE;
+}
+
 #ifndef PNTF_BUILD_INFO
 #define PNTF_BUILD_INFO "unstamped"
 #endif
@@ -227,14 +240,15 @@ static int run_field(int kind, const float* packed, int dim, const float* xp, in
   if (n == 0) return PNTF_OK;
   if (!out0 || (kind == K_TAU_GRAD && !out1)) return fail(PNTF_ERR_ARG, "null output%s");
   const bool grad = kind != K_TAU && kind != K_TRAVEL;
-  if (use_quad(n, schedule)) {   // σ10 stays in LDS: no workspace
+  const int resolved = resolve_field_schedule(n, schedule);
+  if (resolved == PNTF_SCHED_QUAD_TILE) {   // σ10 stays in LDS: no workspace
     FieldArgs a{packed, xp, Btab, env, n, n_env, mode, out0, out1, (float*)ws};
     if (dim == 3) launch_quad<3>(kind, quad_grid_for(n), a, s);
     else launch_quad<6>(kind, quad_grid_for(n), a, s);
     return check_launch("field_quad_kernel");
   }
-  const bool split = use_split(n, schedule);
-  const bool wide = !split && schedule != PNTF_SCHED_WAVE_TILE;
+  const bool split = resolved == PNTF_SCHED_SPLIT_TILE;
+  const bool wide = resolved == PNTF_SCHED_WIDE_TILE;
   int64_t grid = split ? split_grid_for(n) : wide ? wide_grid_for(n) : grid_for(n);
   if (grad) {
     if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
@@ -271,6 +285,11 @@ int pntf_set_field_schedule(int schedule) {
   if (!valid_schedule(schedule)) return fail(PNTF_ERR_ARG, "unknown schedule%s");
   g_field_schedule = schedule;
   return PNTF_OK;
+}
+
+int pntf_field_schedule_for(int64_t n, int schedule) {
+  if (n < 0 || !valid_schedule(schedule)) return -1;
+  return resolve_field_schedule(n, schedule);
 }
 
 size_t pntf_workspace_bytes(int64_t n) {

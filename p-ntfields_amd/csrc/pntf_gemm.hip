@@ -681,6 +681,15 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
     }
     return PNTF_OK;
   }
+  // the LDS-tiled kernel puts the row tiles on grid.y (HIP limit 65535): M above
+  // 65535 * 128 ≈ 8.4M rows cannot launch there (the panel path above has no such limit)
+  if ((M + BM - 1) / BM > 65535) {
+    snprintf(g_err, sizeof(g_err),
+             "pntf_tt_gemm: M = %lld rows exceeds the LDS-tiled kernel's grid (65535 x %d); "
+             "use the panel path (ta = 0, K, N in {128, 256}, beta 0 or 1, aligned operands)",
+             (long long)M, BM);
+    return PNTF_ERR_ARG;
+  }
   const int64_t s = K > 0 ? splits_for(M, N, K) : 1;
   if (s > 1 && (!work || work_floats < (size_t)(s * M * N))) {
     snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: work buffer too small");

@@ -554,7 +554,9 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = gridDim.x * WAVES;
-  // tile indices are wave-uniform 32-bit values (kept in SGPRs; n < 2^36 pairs)
+  // tile indices are wave-uniform 32-bit values (kept in SGPRs): tile * WTILE must stay below
+  // 2^31, so the host sends batches above 2^31 - 32 pairs to the wave-tile kernel instead
+  // (pntf_capi.hip WIDE_MAX_PAIRS)
   const int ntiles = (int)((a.n + WTILE - 1) / WTILE);
   const WScratch sc =
       make_wscratch(GRAD ? a.ws + (int64_t)slot * WSCRATCH_FLOATS_PER_WAVE : nullptr);

@@ -28,6 +28,7 @@ SIGNATURES = {
     "pntf_pack_weights": (ctypes.c_int, [ctypes.POINTER(_c_void_p), ctypes.c_int, _c_void_p,
                                          _c_void_p]),
     "pntf_workspace_bytes": (_size, [_i64]),
+    "pntf_field_schedule_for": (ctypes.c_int, [_i64, ctypes.c_int]),
     "pntf_set_field_schedule": (ctypes.c_int, [ctypes.c_int]),
     "pntf_build_info": (ctypes.c_char_p, []),
     "pntf_field_ex": (ctypes.c_int, [ctypes.c_int, _c_void_p, ctypes.c_int, _c_void_p, _i64,

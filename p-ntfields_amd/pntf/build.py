@@ -7,8 +7,12 @@ beside them; the shared library lands next to this file (p-ntfields_amd/pntf/lib
 it travels with the repo snapshot to the GPU box.  A stamp of the sources and flags skips the
 rebuild when nothing changed.
 
-Two codegen guards fail the build instead of shipping a wrong kernel:
-  * no VGPR spills (a spilling build of the field kernel corrupted results, DESIGN.md §7);
+Codegen guards fail the build instead of shipping a wrong kernel:
+  * no scratch use and no VGPR spills (a spilling build of the field kernel corrupted results,
+    DESIGN.md §7), except a recorded number of in-register (AGPR) spills for the units of
+    VGPR_SPILL_ALLOWED;
+  * no SGPR spills in the headline wide units (SGPR_SPILL_FREE);
+  * every saved-σ scratch load carries the nt policy (scratch_policy_violations);
   * no packed-fp32 VALU ops (v_pk_{mul,add,fma}_f32) in device code.  On gfx950 a packed op
     that reads the result of a transcendental (v_exp/v_log/v_rcp/v_sin/v_cos) issued a few
     instructions earlier sees stale values in lanes 12-15 of every 16-lane row; ROCm 7.2's
@@ -66,6 +70,10 @@ def scratch_policy_violations(asm):
 # units whose kernels must not spill SGPRs either: the headline τ+∇τ kernel and its τ-only /
 # travel-time siblings (the narrow 16-pair kernels still spill ~24-335 SGPRs to VGPR lanes)
 SGPR_SPILL_FREE = re.compile(r"^wide_d\d_k[014]$")
+# VGPR spills that stay in the register file (to AGPRs, ScratchSize 0) accepted per unit, as
+# measured when the unit was last changed; more than this fails the build.  The SOLO planner
+# holds the VALU-layer accumulators beside the 32-fragment ring.
+VGPR_SPILL_ALLOWED = {"plan_quad_solo_d3": 2, "plan_quad_solo_d6": 2}
 
 UNITS = (
     [("field_d%d_k%d" % (d, k), "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k])
@@ -176,10 +184,11 @@ def _compile(unit, uid=None):
     if r.returncode != 0:
         raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (name, " ".join(cmd), r.stderr))
     res = _resources(r.stderr)
-    # A VGPR "spill" with no scratch is a copy into an AGPR (a register move); spills to
-    # scratch memory are what broke the 2-waves/SIMD build, and those fail the build.
-    bad = {k: v for k, v in res.items() if v.get("ScratchSize [bytes/lane]", 0) or (
-        v.get("VGPRs Spill", 0) and not name.startswith(("wide_", "plan_quad_")))}
+    # Spills to scratch memory are what broke the 2-waves/SIMD build: any scratch use fails.
+    # A VGPR "spill" with no scratch is a copy into an AGPR (a register move); only the units
+    # of VGPR_SPILL_ALLOWED may have them, at most the recorded count.
+    bad = {k: v for k, v in res.items() if v.get("ScratchSize [bytes/lane]", 0) or
+           v.get("VGPRs Spill", 0) > VGPR_SPILL_ALLOWED.get(name, 0)}
     if bad:
         raise RuntimeError("VGPR spills / scratch in %s: %s" % (name, bad))
     if SGPR_SPILL_FREE.match(name):

@@ -19,17 +19,20 @@ def world():
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
-def init(backend=None, device=None):
-    """Initialise the default process group when launched with WORLD_SIZE > 1.
+def init(backend=None, device=None, force=False):
+    """Initialise the default process group when launched with WORLD_SIZE > 1 (or, with
+    `force`, also at world size 1: a one-rank RCCL communicator, so the collective path can be
+    exercised and timed on a single GPU).
 
     backend "nccl" is RCCL on ROCm (over xGMI inside a node); pass the rank's HIP `device`
     (already made current) so the communicator binds to it.  Returns (rank, world_size) as
     the process group reports them, which must equal the environment's."""
     rank, ws, _ = world()
-    if ws > 1 and not dist.is_initialized():
+    if (ws > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
         kw = {"device_id": device} if (device is not None and backend == "nccl") else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=ws, **kw)
     if dist.is_initialized():
@@ -47,12 +50,14 @@ def shard_range(n, rank, world_size):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def all_gather_rows(local, n_total, group=None):
+def all_gather_rows(local, n_total, group=None, force=False):
     """Concatenate every rank's row-slice (shard_range order) into the full (n_total, ...)
     tensor on every rank.  Shards are padded to the largest one so the collective is a
-    single all_gather_into_tensor."""
+    single all_gather_into_tensor.  At world size 1 the local block is returned as is, unless
+    `force` (and a process group exists): then the collective runs anyway (a copy through
+    RCCL), which is how the single-GPU tests and bench exercise and time the RCCL path."""
     ws = dist.get_world_size(group) if dist.is_initialized() else 1
-    if ws == 1:
+    if ws == 1 and not (force and dist.is_initialized()):
         return local
     chunk = -(-n_total // ws)
     if n_total == chunk * ws:                 # equal shards: gather straight into the result

@@ -9,6 +9,7 @@ a slot set, so concurrent calls on different streams cannot overwrite each other
 tiles.  The kernel schedule is an argument of every call (pntf_field_ex); nothing here
 mutates process-wide library state.
 """
+import collections
 import ctypes
 
 import torch
@@ -20,7 +21,33 @@ __all__ = ["GRAD_EXACT", "GRAD_BACKGRAD_COMPAT", "PntfError", "pack_weights", "t
            "tau_grad", "path_velocity", "speed", "travel_time", "plan", "eikonal_residual",
            "device_sum", "packed_floats", "workspace_bytes", "point_mesh_distance"]
 
-_ws_cache = {}
+class StreamScratch:
+    """Grow-only device scratch per (device, stream), least-recently-used first out.
+
+    A buffer is recorded on the stream it serves, so the caching allocator keeps its memory
+    alive until that stream's queued work is done even after the entry is dropped or
+    replaced.  At most `cap` streams keep a buffer: a caller that cycles through short-lived
+    streams does not pin one buffer per dead stream, and a recycled stream handle at worst
+    reuses a live buffer of the right size."""
+
+    def __init__(self, dtype, cap=8):
+        self.dtype, self.cap = dtype, cap
+        self.entries = collections.OrderedDict()
+
+    def get(self, device, numel):
+        stream = torch.cuda.current_stream(device)
+        key = (device.index, stream.cuda_stream)
+        buf = self.entries.pop(key, None)
+        if buf is None or buf.numel() < numel:
+            buf = torch.empty(max(int(numel), 1), dtype=self.dtype, device=device)
+            buf.record_stream(stream)
+        self.entries[key] = buf
+        while len(self.entries) > self.cap:
+            self.entries.popitem(last=False)
+        return buf
+
+
+_ws_cache = StreamScratch(torch.uint8)
 
 
 def _vp(t):
@@ -46,18 +73,9 @@ def workspace_bytes(n):
 
 
 def _workspace(device, n):
-    """Grow-only scratch buffer per (device, stream) (saved σ10 tiles of the reverse sweep).
-    Memory is recorded on the stream it serves, so the caching allocator keeps it alive until
-    that stream's work is done even when a larger buffer replaces it."""
-    need = workspace_bytes(n)
-    stream = torch.cuda.current_stream(device)
-    key = (device.index, stream.cuda_stream)
-    ws = _ws_cache.get(key)
-    if ws is None or ws.numel() < need:
-        ws = torch.empty(need, dtype=torch.uint8, device=device)
-        ws.record_stream(stream)
-        _ws_cache[key] = ws
-    return ws
+    """Scratch buffer per (device, stream) for the saved σ10 tiles of the reverse sweep
+    (StreamScratch: grow-only, LRU over streams)."""
+    return _ws_cache.get(device, workspace_bytes(n))
 
 
 def pack_weights(params, out=None):
@@ -103,6 +121,14 @@ def _prep(xp, Btab, env, dim):
 
 SCHEDULES = {"auto": 0, "wave_tile": 1, "split_tile": 2, "wide_tile": 3, "quad_tile": 4}
 FIELD_TAU, FIELD_TAU_GRAD, FIELD_VELOCITY, FIELD_SPEED, FIELD_TRAVEL = range(5)
+
+
+def resolved_schedule(n, schedule="auto"):
+    """Name of the kernel family a field call of n pairs runs (pntf_field_schedule_for)."""
+    r = int(_lib.load().pntf_field_schedule_for(int(n), _sched(schedule)))
+    if r < 0:
+        raise PntfError("bad batch size or schedule")
+    return {v: k for k, v in SCHEDULES.items()}[r]
 
 
 def _sched(schedule):

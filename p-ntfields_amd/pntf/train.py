@@ -49,35 +49,20 @@ def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-_partial_cache = {}
+_partial_cache = ops.StreamScratch(torch.float32)
 
 
 def _partial(device):
     """Reduction scratch per (device, stream): calls on different streams never share it."""
-    stream = torch.cuda.current_stream(device)
-    key = (device.index, stream.cuda_stream)
-    buf = _partial_cache.get(key)
-    if buf is None:
-        buf = torch.empty(int(_lib.load().pntf_tt_partial_floats()), dtype=torch.float32,
-                          device=device)
-        buf.record_stream(stream)
-        _partial_cache[key] = buf
-    return buf
+    return _partial_cache.get(device, int(_lib.load().pntf_tt_partial_floats()))
 
 
-_work_cache = {}
+_work_cache = ops.StreamScratch(torch.float32)
 
 
 def _work(device, floats):
     """Split-K partial sums of pntf_tt_gemm per (device, stream), grown on demand."""
-    stream = torch.cuda.current_stream(device)
-    key = (device.index, stream.cuda_stream)
-    buf = _work_cache.get(key)
-    if buf is None or buf.numel() < floats:
-        buf = torch.empty(max(int(floats), 1), dtype=torch.float32, device=device)
-        buf.record_stream(stream)
-        _work_cache[key] = buf
-    return buf
+    return _work_cache.get(device, floats)
 
 
 def gemm(C, A, B, ta, tb, beta=0.0):

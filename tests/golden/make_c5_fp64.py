@@ -1,0 +1,46 @@
+"""fp64 adjudication of the C5 workload (VERDICT r02 "Next" item 1.3).
+
+    python tests/golden/make_c5_fp64.py
+
+Runs the fp64 oracle planner (oracle/pntf_oracle.plan, a restatement of test/arm_plan.py:140-152
+on models/model_res_sigmoid.py:1247-1282) over the 1024 C5 queries at the reference-written W2
+arm checkpoint (ckpt_w2_d6.pt) and stores its iteration counts and final states beside the
+reference's own fp32 batch-1 loops (plan_c5_w2.npz).  tests/test_w2.py then judges the HIP
+planner query by query against the spread between the fp32 reference and this fp64 run, not
+against a blanket bound.  Needs only the repo (no reference import); ~10 min on 8 cores.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import pntf_oracle as O  # noqa: E402
+
+
+def main():
+    ck = torch.load(os.path.join(HERE, "ckpt_w2_d6.pt"), map_location="cpu", weights_only=True)
+    W = {k: v.numpy().astype(np.float32) for k, v in ck["model_state_dict"].items()}
+    B = ck["B_state_dict"].numpy().T                     # (6, 128): the arm's B.T
+    c = np.load(os.path.join(HERE, "plan_c5_w2.npz"))
+    t0 = time.time()
+    path, steps = O.plan(W, c["xq"], B, dim=6, step=float(c["step"]), tol=float(c["tol"]),
+                         max_iter=int(c["max_iter"]), compat=False)
+    q = np.arange(len(steps))
+    final = path[q, steps]
+    ref_err = np.abs(final - c["final"]).max(1)
+    print("fp64 plan %.0f s: mean %.1f max %d steps; iteration counts differing from the fp32 "
+          "reference: %d; ref-vs-fp64 final error p99 %.2e max %.2e"
+          % (time.time() - t0, steps.mean(), steps.max(), int((steps != c["iters"]).sum()),
+             np.quantile(ref_err, 0.99), ref_err.max()))
+    np.savez_compressed(os.path.join(HERE, "plan_c5_w2_fp64.npz"), iters=steps.astype(np.int32),
+                        final=final, weight_checksum=c["weight_checksum"])
+
+
+if __name__ == "__main__":
+    main()

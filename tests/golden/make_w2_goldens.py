@@ -24,6 +24,9 @@ reference the same way as make_goldens.py:
 3. c5: the C5 workload (1024 arm queries, synth.make_box_pairs(1024, 6, seed=3), step 0.015,
    tol 0.03) as 1024 independent batch-1 reference loops capped at 199 steps (the bench's
    max_iter): iteration counts, final states and the first 16 full paths.
+4. train_grads: at the same reloaded checkpoints, the reference's training step on batches of
+   the trained field — every parameter's `loss.backward()` gradient and selected parameters
+   after two AdamW steps (train_w2_d{3,6}.npz; make_train_goldens.py's recorder).
 
 Only inputs and outputs (data) and the reference-written checkpoints are stored.
 """
@@ -285,12 +288,65 @@ def goldens_c5(ma, out, log, q=1024, cap=199, keep=16):
                         max_iter=np.int32(cap), weight_checksum=csum)
 
 
+def goldens_train(md, ma, out, log):
+    """The reference's training step at the trained weights:
+    `loss.backward()` gradients of every parameter and selected parameters after two
+    torch.optim.AdamW steps (models/model_res_sigmoid_multi.py:1070-1080; arm
+    models/model_res_sigmoid.py:1065-1075), on batches of the analytic field the weights were
+    trained on, so the saturated-softplus regime of the Taylor adjoint is exercised."""
+    from make_train_goldens import _step_record
+    import torch
+    model = md.Model(out, ".", 3, 2, device="cpu")
+    model.load(os.path.join(out, "ckpt_w2_d3.pt"))
+    net = model.network
+    net.train()
+    W = state_np(net)
+    keys = list(W.keys())
+    E, npe = 2, 96
+    Bt = synth.make_B_table(E, 3, first_seed=41)
+    fields = [sphere_field(3, 6, 51 + e, 1.0) for e in range(E)]
+    pts = synth.make_pairs(E * npe, 3, seed=91).reshape(E, npe, 6)
+    yobs = np.stack([field_speeds(pts[e], fields[e], 3) for e in range(E)])
+    sat = saturation(W, pts.reshape(-1, 6), Bt[0], 3)
+
+    def loss_d3():
+        x = to_t(pts).requires_grad_()
+        return model.Loss(x, to_t(yobs), to_t(Bt), 1.0, 1e-3)
+    rec = _step_record(model, net, loss_d3, keys)
+    np.savez_compressed(os.path.join(out, "train_w2_d3.npz"), pts=pts, yobs=yobs, B_table=Bt,
+                        beta=np.float64(1.0), gamma=np.float64(1e-3),
+                        weight_checksum=weight_checksum(W), softplus_saturation=np.float64(sat),
+                        versions=np.array([torch.__version__, np.__version__]), **rec)
+    log("train W2 d3: loss_n %.5f, saturation %.4f" % (float(rec["loss_n"]), sat))
+    amodel = arm_model(ma, out)
+    anet = amodel.network
+    anet.train()
+    Wa = state_np(anet)
+    Ba = amodel.B.detach().numpy().astype(np.float32)
+    field = sphere_field(6, 8, 62, 1.5)
+    na = 128
+    pts_a = synth.make_box_pairs(na, 6, seed=92)
+    yobs_a = field_speeds(pts_a, field, 6)
+    sat = saturation(Wa, pts_a, Ba.T, 6)
+
+    def loss_d6():
+        x = to_t(pts_a).requires_grad_()
+        return amodel.Loss(x, to_t(yobs_a), 1.0, 1e-3)
+    rec = _step_record(amodel, anet, loss_d6, list(Wa.keys()))
+    np.savez_compressed(os.path.join(out, "train_w2_d6.npz"), pts=pts_a, yobs=yobs_a, B=Ba,
+                        beta=np.float64(1.0), gamma=np.float64(1e-3),
+                        weight_checksum=weight_checksum(Wa), softplus_saturation=np.float64(sat),
+                        versions=np.array([torch.__version__, np.__version__]), **rec)
+    log("train W2 d6: loss_n %.5f, saturation %.4f" % (float(rec["loss_n"]), sat))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--stage", default="all", choices=["all", "train", "goldens", "c5"])
+    ap.add_argument("--stage", default="all",
+                    choices=["all", "train", "goldens", "c5", "train_grads"])
     args = ap.parse_args()
     import torch
     torch.manual_seed(0)
@@ -309,6 +365,8 @@ def main():
         goldens_arm(ma, args.out, log)
     if args.stage in ("all", "c5"):
         goldens_c5(ma, args.out, log)
+    if args.stage in ("all", "train_grads"):
+        goldens_train(md, ma, args.out, log)
     log("done")
 
 

@@ -286,3 +286,39 @@ def test_scratch_guard_catches_a_build_without_nt_loads(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     descs, good, bad = build.scratch_policy_violations(open(out).read())
     assert descs and bad > 0 and good == 0, (descs, good, bad)
+
+
+def test_field_schedule_resolution_and_wide_index_guard():
+    """AUTO's kernel choice (include/pntf.h), and the guard of ADVICE r02: the wide kernel
+    keeps 32-bit tile indices, so no batch above 2^31 - 32 pairs may reach it, whatever
+    schedule is asked for (those run the int64-indexed wave-tile kernel).  Host-only: without
+    a GPU the CU count is 256."""
+    L = _lib.load()
+    AUTO, WAVE, SPLIT, WIDE, QUAD = range(5)
+    cus = 256
+    assert L.pntf_field_schedule_for(1, AUTO) == QUAD
+    assert L.pntf_field_schedule_for(4 * cus, AUTO) == QUAD
+    assert L.pntf_field_schedule_for(4 * cus + 1, AUTO) == SPLIT
+    assert L.pntf_field_schedule_for(32 * cus, AUTO) == SPLIT
+    assert L.pntf_field_schedule_for(32 * cus + 1, AUTO) == WIDE
+    assert L.pntf_field_schedule_for(1 << 20, AUTO) == WIDE
+    lim = (1 << 31) - 32
+    for sched in (AUTO, WIDE):
+        assert L.pntf_field_schedule_for(lim, sched) == WIDE
+        assert L.pntf_field_schedule_for(lim + 1, sched) == WAVE
+        assert L.pntf_field_schedule_for(1 << 33, sched) == WAVE
+    assert L.pntf_field_schedule_for(1 << 20, WAVE) == WAVE
+    assert L.pntf_field_schedule_for(1 << 20, SPLIT) == SPLIT
+    assert L.pntf_field_schedule_for(5, QUAD) == QUAD
+    assert L.pntf_field_schedule_for(-1, AUTO) == -1 and L.pntf_field_schedule_for(4, 9) == -1
+
+
+def test_gemm_rejects_rows_beyond_lds_tiled_grid_without_gpu():
+    """the LDS-tiled GEMM puts row tiles on grid.y (limit 65535); an M past
+    65535 * 128 rows on that path is rejected with a clear error before any launch."""
+    L = _lib.load()
+    fake = ctypes.c_void_p(256)
+    M = 65535 * 128 + 1
+    st = L.pntf_tt_gemm(1, 0, M, 128, 256, fake, M, fake, 128, fake, 128, 0.0, fake, 1 << 40,
+                        None)
+    assert st == 1 and b"grid" in L.pntf_tt_gemm_last_error()

@@ -62,3 +62,23 @@ def test_shard_range_partitions():
 def test_gloo_world2_gather(n, q):
     port = _free_port()
     mp.start_processes(_worker, args=(2, port, n, q), nprocs=2, join=True, start_method="spawn")
+
+
+def _worker_ws1(_rank, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                      WORLD_SIZE="1", LOCAL_RANK="0")
+    import torch.distributed as tdist
+    assert dist.init("gloo") == (0, 1) and not tdist.is_initialized()
+    assert dist.init("gloo", force=True) == (0, 1) and tdist.get_world_size() == 1
+    local = torch.arange(21, dtype=torch.float32).reshape(7, 3)
+    assert dist.all_gather_rows(local, 7) is local               # no collective by default
+    full = dist.all_gather_rows(local, 7, force=True)            # the collective, one rank
+    assert full is not local and torch.equal(full, local)
+    tdist.destroy_process_group()
+
+
+def test_gloo_world1_forced_collective():
+    """`force` runs the real collective at world size 1 (the path the GPU test
+    test_rccl.py::test_rccl_world1_allgather drives over RCCL)."""
+    mp.start_processes(_worker_ws1, args=(_free_port(),), nprocs=1, join=True,
+                       start_method="spawn")

@@ -121,3 +121,21 @@ def test_arm_laplace_and_loss_variant(W):
     assert rel_l2(ltau, f["ltau"]) < 1e-4
     assert rel_l2(diff, f["diff"]) < 1e-4
     assert abs(diff.sum() / len(diff) - float(f["loss_n"])) < 1e-5
+
+
+@pytest.mark.parametrize("name", ["fwd_grad_d3.npz", "fwd_grad_env_d3.npz", "fwd_grad_d6.npz"])
+def test_torch_ref_cpu_baseline_vs_reference(W, name):
+    """oracle/torch_ref.py (the op sequence bench.py times as cpu_baseline) reproduces the
+    reference's NN.out + Model.gradient outputs: single B, per-pair env table, and the arm
+    (dim 6, B.T).  fp32 on both sides, same torch CPU kernels: agreement at rounding level."""
+    from oracle.torch_ref import TorchRef
+    f = load(name)
+    ref = TorchRef(W)
+    if name == "fwd_grad_d6.npz":
+        t, d = ref.tau_grad(f["xp"], f["B"].T)
+    elif "B_table" in f.files:
+        t, d = ref.tau_grad(f["xp"], f["B_table"], f["env"])
+    else:
+        t, d = ref.tau_grad(f["xp"], f["B"])
+    assert rel_l2(t.numpy(), f["tau"].reshape(-1)) < TOL
+    assert rel_l2(d.numpy(), f["dtau"]) < TOL

@@ -2,7 +2,10 @@
 
 Pinning: tests/golden/train_d{3,6}.npz hold the reference's own `loss.backward()` gradients
 and its torch.optim.AdamW parameters after two steps (tests/golden/make_train_goldens.py,
-imports the reference).  The CPU tests pin the oracle's hand-derived adjoint
+imports the reference) at the seeded init weights; train_w2_d{3,6}.npz the same at the
+reference-trained W2 checkpoints (make_w2_goldens.py --stage train_grads), on batches of the
+field they were trained on, where 13-16 % of the pre-activations sit on softplus's identity
+branch (the saturated regime of the Taylor-tape adjoint).  The CPU tests pin the oracle's hand-derived adjoint
 (oracle.eikonal_loss_grad) to them; the GPU tests compare the HIP Taylor-tape path with
 both.  Tolerance: each parameter's gradient within 2e-4 of the golden relative to that
 parameter's max |gradient| (fp32 GEMM sums over up to 13·n Taylor rows).  AdamW itself is
@@ -11,11 +14,13 @@ steps from the reference's state: Adam normalises every coordinate (|update| ≈
 the gradient's size), so a near-zero gradient whose fp32 rounding differs can move a weight
 by up to 2·lr per step; 99 % of the weights must agree within 1e-6 and all within 4·lr.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from golden_util import load, weights
+from golden_util import GOLDEN, load, weight_checksum, weights
 from oracle import pntf_oracle as O
 from pntf import synth
 
@@ -28,9 +33,26 @@ def _rel(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 
+CASES = [("train_d3.npz", 3), ("train_d6.npz", 6), ("train_w2_d3.npz", 3),
+         ("train_w2_d6.npz", 6)]
+
+
+def _case_weights(name):
+    """Seeded init weights (train_d*.npz) or the reference-written trained checkpoint the
+    train_w2_d*.npz fixture was recorded at (tests/golden/make_w2_goldens.py train_grads)."""
+    if "w2" not in name:
+        return weights()
+    dim = 3 if name.endswith("d3.npz") else 6
+    sd = torch.load(os.path.join(GOLDEN, "ckpt_w2_d%d.pt" % dim), map_location="cpu",
+                    weights_only=True)["model_state_dict"]
+    W = {k: v.numpy().astype(np.float32) for k, v in sd.items()}
+    assert np.array_equal(weight_checksum(W), load(name)["weight_checksum"])
+    return W
+
+
 def _golden_case(name):
     f = load(name)
-    if name == "train_d3.npz":
+    if name.endswith("d3.npz"):
         E, n = f["pts"].shape[:2]
         xp = f["pts"].reshape(E * n, -1)
         yobs = f["yobs"].reshape(E * n, 2)
@@ -44,9 +66,9 @@ def _golden_case(name):
 # ---------------------------------------------------------------- CPU: oracle pinned
 
 
-@pytest.mark.parametrize("name", ["train_d3.npz", "train_d6.npz"])
+@pytest.mark.parametrize("name", [c[0] for c in CASES])
 def test_oracle_weight_grads_vs_reference(name):
-    W = weights()
+    W = _case_weights(name)
     f, c = _golden_case(name)
     B = c["B"][0] if c["env"] is None else c["B"]
     diff, g = O.eikonal_loss_grad(W, c["xp"], c["yobs"], B, c["env"], c["dim"],
@@ -100,10 +122,10 @@ def _loss(model, f, dim, dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,dim", [("train_d3.npz", 3), ("train_d6.npz", 6)])
+@pytest.mark.parametrize("name,dim", CASES)
 def test_loss_backward_vs_reference(name, dim):
     dev = torch.device("cuda:0")
-    W = weights()
+    W = _case_weights(name)
     f = load(name)
     model, net = _nets(dim, W, dev, f["B"] if dim == 6 else None)
     loss, loss_n, diff = _loss(model, f, dim, dev)
@@ -119,11 +141,11 @@ def test_loss_backward_vs_reference(name, dim):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,dim", [("train_d3.npz", 3), ("train_d6.npz", 6)])
+@pytest.mark.parametrize("name,dim", CASES)
 def test_two_adamw_steps_vs_reference(name, dim):
     from pntf.train import AdamW
     dev = torch.device("cuda:0")
-    W = weights()
+    W = _case_weights(name)
     f = load(name)
     model, net = _nets(dim, W, dev, f["B"] if dim == 6 else None)
     opt = AdamW(net.parameters(), lr=1e-3, weight_decay=0.1)

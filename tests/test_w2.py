@@ -231,37 +231,66 @@ def test_w2_planners_vs_reference(multi, arm, schedule):
     assert np.abs(path.cpu().numpy() - a["paths"]).max() < 1e-3
 
 
+def c5_envelope_check(steps, fin, ref_iters, ref_final, f64_iters, f64_final, tol=1e-3):
+    """Query-by-query judgement of a C5 run.  Over 100-200 planner
+    steps through a trained field, fp32 summation-order differences are amplified on a few
+    trajectories; the fp64 oracle (plan_c5_w2_fp64.npz) says how far the fp32 reference itself
+    is from the exact plan on each query.  Every query must
+      * stop at an iteration count between the reference's and the fp64 plan's (inclusive),
+      * end within `tol` + 2·spread of the final state of a plan (reference or fp64) that
+        stopped at the same count, spread = |reference - fp64| on that query.
+    Returns the per-query error and spread."""
+    lo, hi = np.minimum(ref_iters, f64_iters), np.maximum(ref_iters, f64_iters)
+    bad = np.nonzero((steps < lo) | (steps > hi))[0]
+    assert bad.size == 0, ("iteration counts outside the ref/fp64 envelope", bad.tolist(),
+                           steps[bad].tolist(), ref_iters[bad].tolist(), f64_iters[bad].tolist())
+    spread = np.abs(ref_final - f64_final).max(1)
+    inf = np.full(len(steps), np.inf)
+    e_ref = np.where(steps == ref_iters, np.abs(fin - ref_final).max(1), inf)
+    e_64 = np.where(steps == f64_iters, np.abs(fin - f64_final).max(1), inf)
+    err = np.minimum(e_ref, e_64)
+    worst = np.nonzero(err > tol + 2 * spread)[0]
+    assert worst.size == 0, ("final states outside the envelope", worst.tolist(),
+                             err[worst].tolist(), spread[worst].tolist())
+    return err, spread
+
+
+def test_c5_fp64_adjudication_fixture():
+    """plan_c5_w2_fp64.npz (tests/golden/make_c5_fp64.py): the fp64 oracle at the same
+    checkpoint; it agrees with the fp32 reference to 1e-3 on all but a handful of long
+    trajectories, and those are where the reference's own iteration counts drift."""
+    c, f = load("plan_c5_w2.npz"), load("plan_c5_w2_fp64.npz")
+    np.testing.assert_array_equal(f["weight_checksum"], c["weight_checksum"])
+    spread = np.abs(f["final"] - c["final"]).max(1)
+    assert (spread > 1e-3).sum() <= 8 and (f["iters"] != c["iters"]).sum() <= 8
+    # the envelope check accepts the reference itself and the fp64 plan itself
+    c5_envelope_check(c["iters"], c["final"], c["iters"], c["final"], f["iters"], f["final"])
+    c5_envelope_check(f["iters"], f["final"], c["iters"], c["final"], f["iters"], f["final"])
+
+
 @pytest.mark.gpu
 def test_w2_c5_1024_queries_vs_reference(arm):
     """C5 at full size: 1024 arm queries, ≤199 steps, per-query freeze (Model.Plan, the
     bench's planner call) vs 1024 independent reference batch-1 loops (test/arm_plan.py) at
-    trained weights, where plans run 100-200 steps.  Both sides are fp32 and differ in
-    summation order, so a query whose distance crosses tol within rounding of the stop test
-    may stop a few steps apart: at least 99 % of the iteration counts must be identical (any
-    other within 8 steps — measured: 3 of 1024 differ on quad tiles, by 5, 3 and 1, on
-    trajectories of 118, 78 and 44 steps — with its own stop taken legitimately at
-    |xg - xs| <= tol); 99 % of
-    the identical-count final states within 1e-3 (all within 2e-2: a few long trajectories
-    amplify rounding), the 16 stored full paths within 1e-3."""
+    trained weights, where plans run 100-200 steps, judged query by query against the fp64
+    oracle's plan (c5_envelope_check): every iteration count between the reference's and the
+    fp64 one, every final state within 1e-3 + 2·(reference - fp64 spread) of a plan that
+    stopped at the same count; 99 % of the iteration counts equal the reference's and 99 % of
+    the final states within 1e-3 of it; the 16 stored full paths within 1e-3."""
     dev = torch.device("cuda:0")
-    c = load("plan_c5_w2.npz")
+    c, f64 = load("plan_c5_w2.npz"), load("plan_c5_w2_fp64.npz")
     tol = float(c["tol"])
     path, steps = arm.Plan(_T(c["xq"], dev), step=0.015, tol=tol, max_iter=int(c["max_iter"]))
     path, steps = path.cpu().numpy(), steps.cpu().numpy()
-    ref = c["iters"]
-    same = steps == ref
-    assert same.mean() >= 0.99, (int((~same).sum()), np.nonzero(~same)[0][:10].tolist())
-    assert np.abs(steps - ref).max() <= 8, (np.nonzero(~same)[0].tolist(),
-                                            (steps - ref)[~same].tolist(), ref[~same].tolist())
     q = np.arange(len(steps))
     fin = path[q, steps]
     dist = np.linalg.norm(fin[:, 6:] - fin[:, :6], axis=1)
     assert np.all((dist <= tol) | (steps > int(c["max_iter"])))
-    # 100-200 steps through a trained field amplify fp32 summation-order differences on a few
-    # trajectories: 99 % of the same-count final states within 1e-3, all within 2e-2
-    err = np.abs(fin[same] - c["final"][same]).max(1)
-    assert np.quantile(err, 0.99) < 1e-3 and err.max() < 2e-2, (
-        float(np.quantile(err, 0.99)), float(err.max()), int((err > 1e-3).sum()))
+    err, spread = c5_envelope_check(steps, fin, c["iters"], c["final"], f64["iters"],
+                                    f64["final"])
+    same = steps == c["iters"]
+    assert same.mean() >= 0.99, (int((~same).sum()), np.nonzero(~same)[0][:10].tolist())
+    assert np.quantile(err, 0.99) < 1e-3, float(np.quantile(err, 0.99))
     s16 = same[:16]
     assert np.abs(path[:16][s16] - c["paths16"][s16]).max() < 1e-3
 

@@ -38,8 +38,13 @@ def main():
           "reference: %d; ref-vs-fp64 final error p99 %.2e max %.2e"
           % (time.time() - t0, steps.mean(), steps.max(), int((steps != c["iters"]).sum()),
              np.quantile(ref_err, 0.99), ref_err.max()))
+    # full fp64 paths of the queries where the fp32 reference drifts (iteration count or final
+    # state off by more than 1e-4): a HIP run may stop at any count between the two, and is
+    # then judged against the fp64 state after that many steps
+    drift = np.nonzero((steps != c["iters"]) | (ref_err > 1e-4))[0].astype(np.int32)
     np.savez_compressed(os.path.join(HERE, "plan_c5_w2_fp64.npz"), iters=steps.astype(np.int32),
-                        final=final, weight_checksum=c["weight_checksum"])
+                        final=final, drift=drift, drift_paths=path[drift],
+                        weight_checksum=c["weight_checksum"])
 
 
 if __name__ == "__main__":

@@ -50,12 +50,14 @@ typedef enum {
  *   WIDE_TILE   one wave per 32-pair tile, v_mfma_f32_32x32x2_f32 (pntf_wide.h; throughput,
  *               field entry points only — the planner treats it as WAVE_TILE);
  *   QUAD_TILE   the 4 waves of a workgroup share a 4-pair tile, v_mfma_f32_4x4x1_16b_f32
- *               (pntf_quad.h; lowest latency per planner step, no workspace needed); the
- *               planner runs batches of at most one query per CU (q <= CUs, the reference's
- *               Q = 1 included) one query per workgroup on VALU layers (SOLO; environment
- *               PNTF_QSOLO=0 keeps the MFMA layers);
+ *               (pntf_quad.h; lowest latency per planner step, no workspace needed);
  *   AUTO        quad while ceil(n/4) <= the CU count, split while ceil(n/16) <= 2 x the CU
- *               count, wide above. */
+ *               count, wide above.  For the planner AUTO's quad path also runs batches of at
+ *               most one query per CU (q <= CUs, the reference's Q = 1 included) one query per
+ *               workgroup on VALU layers (SOLO), and larger quad batches hand their last
+ *               <= CUs active queries off to a SOLO launch (tail hand-off; needs 8 + 8q bytes
+ *               of `ws`).  SOLO and the MFMA layers give bit-identical results.  Environment
+ *               PNTF_QSOLO=0 (read once) disables both. */
 #define PNTF_SCHED_AUTO 0
 #define PNTF_SCHED_WAVE_TILE 1
 #define PNTF_SCHED_SPLIT_TILE 2

@@ -428,19 +428,35 @@ int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, cons
   if (q == 0) return PNTF_OK;
   if (!path || !steps) return fail(PNTF_ERR_ARG, "null output%s");
   PlanArgs a{packed, xp0, Btab, env, q, n_env, mode, step, tol, max_iter, path, steps,
-             (float*)ws};
-  if (use_quad(q, schedule)) {   // no workspace
+             (float*)ws, nullptr, 0};
+  if (use_quad(q, schedule)) {
+    const int64_t cus = num_cus();
     dim3 g((unsigned)quad_grid_for(q)), b(256);
-    if (q <= (int64_t)num_cus() && solo_enabled()) {
+    if (schedule == PNTF_SCHED_AUTO && q <= cus && solo_enabled()) {
       // one query per CU (the reference's Q = 1 loop, small batches): VALU SOLO layers
       dim3 gs((unsigned)q);
       if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3, true>), gs, b, 0, stream, a);
       else hipLaunchKernelGGL((plan_quad_kernel<6, true>), gs, b, 0, stream, a);
       return check_launch("plan_quad_kernel<solo>");
     }
+    // AUTO with a workspace: the 4-query tiles hand the last <= CUs active queries off to a
+    // SOLO launch (pntf_quad.h "Tail hand-off"; bit-identical results, QUAD_TILE runs without)
+    const bool hand_off = schedule == PNTF_SCHED_AUTO && solo_enabled() && ws &&
+                          ws_bytes >= sizeof(int32_t) * (size_t)(2 + 2 * q);
+    if (hand_off) {
+      a.tail = (int32_t*)ws;
+      a.yield_at = (int32_t)cus;
+      if (hipMemsetAsync(ws, 0, 2 * sizeof(int32_t), stream) != hipSuccess)
+        return check_launch("plan tail reset");
+    }
     if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3, false>), g, b, 0, stream, a);
     else hipLaunchKernelGGL((plan_quad_kernel<6, false>), g, b, 0, stream, a);
-    return check_launch("plan_quad_kernel");
+    st = check_launch("plan_quad_kernel");
+    if (st || !hand_off) return st;
+    dim3 gs((unsigned)(q < cus ? q : cus));
+    if (dim == 3) hipLaunchKernelGGL((plan_quad_kernel<3, true>), gs, b, 0, stream, a);
+    else hipLaunchKernelGGL((plan_quad_kernel<6, true>), gs, b, 0, stream, a);
+    return check_launch("plan_quad_kernel<solo, resume>");
   }
   if (!ws) return fail(PNTF_ERR_WORKSPACE, "null workspace%s");
   const bool split = use_split(q, schedule);

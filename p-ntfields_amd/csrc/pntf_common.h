@@ -165,6 +165,12 @@ struct PlanArgs {
   float* path;           // (q, max_iter + 2, 2*DIM)
   int32_t* steps;        // (q)
   float* ws;
+  // Tail hand-off of the quad planner (pntf_quad.h; NULL = off): tail[0] = queries done,
+  // tail[1] = queries handed off, tail[2 .. 2+q) = their indices, tail[2+q .. 2+2q) = the
+  // iteration each resumes at.  The 4-query tiles yield once at most `yield_at` queries of the
+  // batch are still active; a SOLO launch with the same `tail` resumes the handed-off ones.
+  int32_t* tail;
+  int32_t yield_at;
 };
 
 struct ResidualArgs {

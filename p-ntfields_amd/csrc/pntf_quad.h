@@ -175,8 +175,11 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
     });
     float v[NC];
     // the compact value of lane l is row r0 + 4·og + kb (the MFMA path's layout): take it
-    // from the lane of the same og whose (l & 3) is this lane's kb
-    const int src_lane = (cx.lane & 0x30) | cx.kb;
+    // from the lane of the same og whose row (l & 3) is this lane's kb AND whose k sub-block
+    // is kb too — there the dpp sums added the four sub-blocks in the order the MFMA path uses
+    // for row kb, so SOLO and the MFMA layers give bit-identical results (the planner's tail
+    // hand-off switches a query from one to the other mid-plan)
+    const int src_lane = (cx.lane & 0x30) | (cx.kb << 2) | cx.kb;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       float t = acc[c][0];
@@ -527,10 +530,27 @@ __global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
 // query per CU): the tile is a single query, loaded into all four pair slots; the layers run
 // as VALU dot products for pair slot 0 (qlayer), the other slots carry the same values, and
 // only slot 0 stores.
+//
+// Tail hand-off (a.tail != NULL): a 4-query tile costs ~57 µs per step on its
+// CU whatever number of its queries are still active, a SOLO query ~43 µs (the per-CU weight
+// stream).  The MFMA tiles count converged queries in tail[0] (device-scope atomics); once at
+// most a.yield_at queries of the batch remain (one per CU), every tile that still has active
+// queries hands them off — index and resume iteration into tail[] — and exits; the SOLO
+// launch that follows resumes each from its path row, one query per workgroup.  The layers
+// are bit-identical in both forms (qlayer), so the plan does not depend on when the hand-off
+// happens.
+constexpr int Q_YIELD_FLAG = Q_BW + QPAIRS * 6 * H;   // LDS word: this tile yields
+static_assert(Q_YIELD_FLAG < Q_LDS_FLOATS, "quad LDS budget");
+
 template <int DIM, bool SOLO>
 __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
   __shared__ float smem[Q_LDS_FLOATS];
   const QCx cx = quad_cx((lds_f*)smem);
+  int32_t* const tail = a.tail;
+  const bool resume = SOLO && tail != nullptr;    // second launch: the handed-off queries
+  const bool can_yield = !SOLO && tail != nullptr;
+  int32_t* const tail_q = tail ? tail + 2 : nullptr;
+  int32_t* const tail_it = tail ? tail + 2 + a.q : nullptr;
   const Rsrc W = make_rsrc(a.P + OFF_QUAD + cx.w * Q_STREAM, Q_STREAM * 4);
   const Rsrc AX = make_rsrc(a.P + OFF_QUAD + Q_OFF_AUX + cx.w * Q_NAUX * 256, Q_NAUX * 1024);
   f32x4 aux[Q_NAUX];
@@ -544,15 +564,15 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
   const int cap = a.max_iter + 1;
   const int64_t rows = (int64_t)cap + 1;
   constexpr int TQ = SOLO ? 1 : QPAIRS;   // queries per tile
-  const int64_t ntiles = (a.q + TQ - 1) / TQ;
+  const int64_t ntiles = resume ? (int64_t)tail[1] : (a.q + TQ - 1) / TQ;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t qi = SOLO ? tile : tile * QPAIRS + (cx.lane & 3);
+    const int64_t qi = resume ? (int64_t)tail_q[tile] : SOLO ? tile : tile * QPAIRS + (cx.lane & 3);
     PairIO io;
     const bool ok = load_pair<DIM>(a.xp0, a.Btab, a.env, a.q, a.n_env, qi, io);
     quad_stage_b<DIM>(cx, io);
     qsync();
     const bool store = cx.w == 0 && cx.lane < TQ && qi < a.q;
-    float* prow = a.path + (store ? qi : 0) * rows * 2 * DIM;
+    float* prow = a.path + (qi < a.q ? qi : 0) * rows * 2 * DIM;
     auto dist = [&]() {
       float s = 0.f;
 #pragma unroll
@@ -562,22 +582,44 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
       }
       return sqrtf(s);
     };
-    bool active = ok && dist() > a.tol;
-    if (store) {
+    int nsteps = 0;
+    int it = 0;
+    bool active;
+    if (resume) {   // continue from the state the MFMA tile left in the path
+      it = tail_it[qi];
+      nsteps = a.steps[qi];
+      const float* pr = prow + (int64_t)it * 2 * DIM;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int d = 0; d < DIM; ++d) prow[c * DIM + d] = io.x[c][d];
+        for (int d = 0; d < DIM; ++d) io.x[c][d] = pr[c * DIM + d];
+      active = true;
+    } else {
+      active = ok && dist() > a.tol;
+      if (store) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int d = 0; d < DIM; ++d) prow[c * DIM + d] = io.x[c][d];
+      }
     }
-    int nsteps = 0;
-    int it = 0;
+    // queries of the batch this tile retires (done from the start: converged, invalid env)
+    auto retire = [&](bool now_done) {
+      const unsigned long long b = __ballot(now_done) & 0xfull;
+      if (cx.w == 0 && cx.lane == 0 && b)
+        __hip_atomic_fetch_add(tail, (int32_t)__builtin_popcountll(b), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (can_yield) retire(qi < a.q && !active);
+    bool yielded = false;
     for (; it < cap; ++it) {
-      if (!__any(active)) break;
+      if (!__any(active) || yielded) break;
       const float tau =
           quad_forward<DIM, true, Q_NF_ALL, QRING, SOLO>(ring, W, cx, io, aux, a.compat);
       float ds[DIM], dg[DIM], vs[DIM], vg[DIM];
       quad_backward<DIM, Q_NF_ALL, QRING, SOLO>(ring, W, cx, io, tau, aux, ds, dg);
       path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
+      bool converged = false;
       if (active) {
 #pragma unroll
         for (int d = 0; d < DIM; ++d) {
@@ -585,7 +627,10 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
           io.x[1][d] = io.x[1][d] + a.step * vg[d];
         }
         ++nsteps;
-        if (!(dist() > a.tol)) active = false;
+        if (!(dist() > a.tol)) {
+          active = false;
+          converged = true;
+        }
       }
       if (store) {
         float* pr = prow + (int64_t)(it + 1) * 2 * DIM;
@@ -594,8 +639,27 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
 #pragma unroll
           for (int d = 0; d < DIM; ++d) pr[c * DIM + d] = io.x[c][d];
       }
+      if (can_yield) {
+        retire(qi < a.q && converged);
+        // one lane reads the batch's done count (device scope, bypasses L1); the decision
+        // goes through LDS so all four waves agree; a yield takes effect at the top of the
+        // next iteration (the state is then path row it + 1)
+        if (cx.w == 0 && cx.lane == 0) {
+          const int32_t done = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          cx.lds[Q_YIELD_FLAG] = a.q - done <= a.yield_at ? 1.f : 0.f;
+        }
+        qsync();
+        yielded = cx.lds[Q_YIELD_FLAG] != 0.f;
+      }
     }
-    if (store) {
+    if (yielded && store && active) {
+      // hand the query off: its state is path row `it`, its step count goes to steps[]
+      const int32_t slot = __hip_atomic_fetch_add(tail + 1, 1, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      tail_q[slot] = (int32_t)qi;
+      tail_it[qi] = it;
+      a.steps[qi] = nsteps;
+    } else if (store) {
       for (int64_t r = it + 1; r < rows; ++r) {
         float* pr = prow + r * 2 * DIM;
 #pragma unroll

@@ -441,3 +441,39 @@ def test_single_query_planner_vs_reference(packed, dev, golden):
         path, steps = ops.plan(packed, T(p["starts"][i:i + 1], dev), B, **kw)
         assert int(steps.cpu()[0]) == int(p["iters"][i]), i
         assert np.abs(path.cpu().numpy()[0] - p["paths"][i]).max() < 1e-3, i
+
+
+@pytest.mark.parametrize("dim,q", [(3, 37), (6, 200)])
+def test_solo_layers_bitwise_equal_mfma_layers(packed, dev, dim, q):
+    """The planner's two quad layer forms give identical bits: AUTO runs batches of at most
+    one query per CU on the SOLO (VALU) layers, QUAD_TILE on the 4x4x1 MFMA layers; same
+    fma chains, same cross-lane sum order (pntf_quad.h qlayer).  This is what lets the C5 tail
+    hand-off move a query from one form to the other mid-plan without changing its path."""
+    xp0 = T(synth.make_box_pairs(q, dim, seed=55 + q), dev)
+    B = synth.make_B(dim, seed=12, arm=dim == 6)
+    B = T(B.T.copy() if dim == 6 else B, dev)
+    kw = dict(dim=dim, step=0.03 if dim == 3 else 0.015, tol=0.06 if dim == 3 else 0.03,
+              max_iter=40, mode=ops.GRAD_BACKGRAD_COMPAT if dim == 3 else ops.GRAD_EXACT)
+    ps, ss = ops.plan(packed, xp0, B, schedule="auto", **kw)
+    pq, sq = ops.plan(packed, xp0, B, schedule="quad_tile", **kw)
+    assert torch.equal(ss, sq)
+    assert torch.equal(ps, pq), float((ps - pq).abs().max())
+
+
+def test_c5_tail_handoff_bitwise_and_taken(packed, dev):
+    """C5 (1024 arm queries, <= 199 steps): AUTO lets the 4-query MFMA tiles hand the last
+    <= CUs active queries to a SOLO launch (pntf_plan_ex); QUAD_TILE keeps them on the tiles.
+    Same bits either way, and the hand-off really happened (the workspace's hand-off count,
+    pntf_common.h PlanArgs::tail, is non-zero)."""
+    q = 1024
+    Ba = T(synth.make_B(6, seed=12, arm=True).T.copy(), dev)
+    xq = T(synth.make_box_pairs(q, 6, seed=3), dev)
+    kw = dict(dim=6, step=0.015, tol=0.03, max_iter=199, mode=ops.GRAD_EXACT)
+    pa, sa = ops.plan(packed, xq, Ba, schedule="auto", **kw)
+    tail = ops._workspace(dev, q)[:8].view(torch.int32).cpu().numpy()
+    pq, sq = ops.plan(packed, xq, Ba, schedule="quad_tile", **kw)
+    assert torch.equal(sa, sq)
+    assert torch.equal(pa, pq), float((pa - pq).abs().max())
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    assert 0 < tail[1] <= cus, tail.tolist()          # handed-off queries
+    assert tail[0] >= q - cus, tail.tolist()          # the done count that triggered it

@@ -551,6 +551,10 @@ __global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
 // are bit-identical in both forms (qlayer), so the plan does not depend on when the hand-off
 // happens.
 constexpr int Q_YIELD_FLAG = Q_BW + QPAIRS * 6 * H;   // LDS word: this tile yields
+#ifndef PNTF_Q_YIELD_EVERY
+#define PNTF_Q_YIELD_EVERY 4
+#endif
+constexpr int Q_YIELD_EVERY = PNTF_Q_YIELD_EVERY;     // steps between hand-off checks (2^k)
 static_assert(Q_YIELD_FLAG < Q_LDS_FLOATS, "quad LDS budget");
 
 template <int DIM, bool SOLO>
@@ -649,11 +653,12 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
 #pragma unroll
           for (int d = 0; d < DIM; ++d) pr[c * DIM + d] = io.x[c][d];
       }
-      if (can_yield) {
-        retire(qi < a.q && converged);
-        // one lane reads the batch's done count (device scope, bypasses L1); the decision
-        // goes through LDS so all four waves agree; a yield takes effect at the top of the
-        // next iteration (the state is then path row it + 1)
+      if (can_yield) retire(qi < a.q && converged);
+      if (can_yield && (it & (Q_YIELD_EVERY - 1)) == Q_YIELD_EVERY - 1) {
+        // every Q_YIELD_EVERY steps one lane reads the batch's done count (device scope,
+        // bypasses L1; its wait drains the weight ring once); the decision goes through LDS so
+        // all four waves agree; a yield takes effect at the top of the next iteration (the
+        // state is then path row it + 1)
         if (cx.w == 0 && cx.lane == 0) {
           const int32_t done = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           cx.lds[Q_YIELD_FLAG] = a.q - done <= a.yield_at ? 1.f : 0.f;

@@ -181,44 +181,47 @@ int pntf_sum(const float* x, int64_t n, double* out, hipStream_t stream);
  * NN.out_laplace (:710-848) layer by layer: each Linear is one plain fp32 library GEMM over
  * all Taylor rows, everything in between is one of the fused kernels below.
  *
- * "Planes": a Taylor tensor of m points and width w is (R, m, w) fp32 with R = 1 + 2*ndir
- * planes [value | ndir first-derivative rows | ndir diagonal second-derivative rows];
- * ndir = dim in the encoder (m = 2n points: the n starts, then the n goals) and 2*dim after
- * the start/goal merge ([d/dx_start (dim) | d/dx_goal (dim)], m = n pairs).
+ * "Planes": a Taylor tensor of m points and width w is (R, m, w) fp32 with R = 1 + ndir + nl
+ * planes [value | ndir first-derivative rows | nl summed second-derivative rows]: (ndir, nl) =
+ * (dim, 1) in the encoder (m = 2n points: the n starts, then the n goals) and (2*dim, 2) after
+ * the start/goal merge ([d/dx_start (dim) | d/dx_goal (dim) | Σ d²/dx_start² | Σ d²/dx_goal²],
+ * m = n pairs).  The loss needs each endpoint's Laplacian only (Model.Loss :919-920), and the
+ * per-direction second-derivative rows of NN.out_laplace enter every layer linearly, so their
+ * per-endpoint sum is carried instead of one row per direction (same loss and gradient).
  * `partial` is caller scratch of pntf_tt_partial_floats() floats (per stream).
  * Errors of these entry points are reported by pntf_tt_last_error.
  * ------------------------------------------------------------------------------------- */
 size_t pntf_tt_partial_floats(void);
 const char* pntf_tt_last_error(void);
 
-/* input_mapping_laplace (:199-213): phi (1 + 2*dim, 2n, 256) = [sin | cos] rows of 2πxB. */
+/* input_mapping_laplace (:199-213): phi (2 + dim, 2n, 256) = [sin | cos] rows of 2πxB. */
 int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, const int32_t* env,
                     int32_t n_env, float* phi, hipStream_t stream);
 
 /* Bias (+ residual) + act_laplace (:663-691, residual :744/:828) on GEMM output y (R, m, w),
- * w = 128|256, ndir = 3|6|12: y's value plane += bias, every plane += res (R, m, w) when res
- * is not NULL (y is kept as the tape); act != 0: h (R, m, w) = softplus10 Taylor rows.
- * act == 0 (Linear without activation, res must be NULL): bias only, h unused. */
-int pntf_tt_act_fwd(int ndir, float* y, float* h, const float* bias, const float* res,
+ * w = 128|256, (ndir, nl) = (3|6, 1) or (6|12, 2): y's value plane += bias, every plane += res
+ * (R, m, w) when res is not NULL (y is kept as the tape); act != 0: h (R, m, w) = softplus10
+ * Taylor rows.  act == 0 (Linear without activation, res must be NULL): bias only, h unused. */
+int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, const float* res,
                     int64_t m, int w, int act, hipStream_t stream);
 
 /* Adjoint of pntf_tt_act_fwd, in place: g (R, m, w) holds dL/dh on entry and dL/dy on exit
  * (act == 0: unchanged); gbias (w) (+)= sum over points of dL/dy's value plane
  * (accumulate != 0 adds to gbias). */
-int pntf_tt_act_bwd(int ndir, const float* y, float* g, int64_t m, int w, int act, float* gbias,
-                    int accumulate, float* partial, hipStream_t stream);
+int pntf_tt_act_bwd(int ndir, int nl, const float* y, float* g, int64_t m, int w, int act,
+                    float* gbias, int accumulate, float* partial, hipStream_t stream);
 
-/* Start/goal merge of the encoder output (:755-811): z (1 + 2*dim, 2n, 128) ->
- * u (1 + 4*dim, n, 256), features [logsumexp max-part | min-part]; and its adjoint
- * gu (1 + 4*dim, n, 256) -> gz (1 + 2*dim, 2n, 128). */
+/* Start/goal merge of the encoder output (:755-811): z (2 + dim, 2n, 128) ->
+ * u (3 + 2*dim, n, 256), features [logsumexp max-part | min-part]; and its adjoint
+ * gu (3 + 2*dim, n, 256) -> gz (2 + dim, 2n, 128). */
 int pntf_tt_merge_fwd(int dim, const float* z, int64_t n, float* u, hipStream_t stream);
 int pntf_tt_merge_bwd(int dim, const float* z, const float* gu, int64_t n, float* gz,
                       hipStream_t stream);
 
 /* generator[4] + actout_laplace (:693-708) + Model.Loss (:897-946; arm = 1: the arm model's
  * square-root variant, models/model_res_sigmoid.py:869-935), forward and backward per pair:
- * v (1 + 4*dim, n, 128) generator[3] output planes, w4 (128), b4 (1) -> diff (n); the
- * gradient of scale * sum(diff): gv (1 + 4*dim, n, 128) w.r.t. v, gw4 (128), gb4 (1). */
+ * v (3 + 2*dim, n, 128) generator[3] output planes, w4 (128), b4 (1) -> diff (n); the
+ * gradient of scale * sum(diff): gv (3 + 2*dim, n, 128) w.r.t. v, gw4 (128), gb4 (1). */
 int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const float* b4,
                       const float* xp, const float* yobs, int64_t n, float gamma, float scale,
                       float* diff, float* gv, float* gw4, float* gb4, float* partial,
@@ -239,14 +242,6 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
                  const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
                  size_t work_floats, hipStream_t stream);
 const char* pntf_tt_gemm_last_error(void);
-
-/* A forward Linear of the Taylor tape fused with pntf_tt_act_fwd (ndir = 3 | 6, R = 1 + 2*ndir
- * planes): y (R, m, n) = x (R, m, k) · Wᵀ (W: n x k), y's value plane += bias, every plane +=
- * res (R, m, n) when res is not NULL; act != 0: h (R, m, n) = softplus10 Taylor rows of y.
- * k a multiple of 16, n a multiple of 128.  Errors: pntf_tt_gemm_last_error. */
-int pntf_tt_linear_act(int ndir, const float* x, int64_t m, int k, const float* w, int n,
-                       const float* bias, const float* res, int act, float* y, float* h,
-                       hipStream_t stream);
 
 /* torch.optim.AdamW update of one parameter tensor (the reference's optimizer, :959-961):
  * p, grad, exp_avg, exp_avg_sq (n); `step` = the step count after this update (>= 1). */

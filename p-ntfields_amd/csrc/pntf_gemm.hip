@@ -434,148 +434,6 @@ __global__ __launch_bounds__(256, PNTF_PANEL_WPS) void panel_gemm_kernel(PanelAr
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Forward Linear of the Taylor tape fused with its epilogue (pntf_tt_linear_act): per point
-// and feature, y planes = x planes · Wᵀ, y₀ += bias, (+ residual planes), then act_laplace
-// (:675-691) h₀ = softplus₁₀(y₀), h_J = σ·J, h_L = σ'·J² + σ·L — the work of pntf_tt_gemm +
-// pntf_tt_act_fwd without the round trip of y through HBM between them.
-// The workgroup's row tile is 32 points × all R planes (R = 1 + 2·ndir ≤ 13), one 32 x 32
-// MFMA row block per plane, so every plane of a (point, feature) lands in the same lane and
-// register of R different accumulators and the cross-plane epilogue runs in registers.
-// 4 waves × 32 features = 128 columns per workgroup; K chunks of 16 through LDS (A stored
-// [k][plane][point]: R odd makes the row stride ≡ 32 mod 64, conflict-free).
-constexpr float TT_SCALE = 10.f;   // Softplus beta (model_res_sigmoid_multi.py:140)
-__device__ __forceinline__ float tt_sig10(float y) { return 1.f / (1.f + expf(-TT_SCALE * y)); }
-__device__ __forceinline__ float tt_softplus10(float y) {
-  return TT_SCALE * y > 20.f ? y : log1pf(expf(TT_SCALE * y)) / TT_SCALE;
-}
-
-struct LinArgs {
-  const float* x;      // (R, M, K)
-  const float* w;      // (N, K)
-  const float* bias;   // (N)
-  const float* res;    // (R, M, N) or null
-  float* y;            // (R, M, N): pre-activation (the tape)
-  float* h;            // (R, M, N): activation (ACT)
-  int64_t M;
-  int N, K;
-};
-
-template <int NDIR, bool ACT, bool RES>
-__global__ __launch_bounds__(256, 1) void tt_linear_act_kernel(LinArgs a) {
-  constexpr int R = 1 + 2 * NDIR, LK = 16;
-  constexpr int AS = R * 32, BS = 160;   // LDS row strides per k (floats)
-  static_assert(R % 2 == 1, "plane count odd: conflict-free A rows");
-  __shared__ float As[2][LK * AS];
-  __shared__ float Bs[2][LK * BS];
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int64_t p0 = (int64_t)blockIdx.x * 32;
-  const int n0 = blockIdx.y * 128;
-  const int64_t plane_x = a.M * a.K, plane_y = a.M * a.N;
-  constexpr int NA = (R * 32 * LK / 4 + 255) / 256;   // float4 loads per thread: A
-  f32x4 ra[NA], rb[2];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = t + 256 * i;   // (plane b, k4, point p), p fastest
-      const int p = idx & 31, k4 = (idx >> 5) & 3, b = idx >> 7;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (b < R && p0 + p < a.M)
-        v = *reinterpret_cast<const f32x4*>(a.x + b * plane_x + (p0 + p) * a.K + k0 + 4 * k4);
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = t + 256 * i;   // (k4, column n), n fastest
-      const int n = idx & 127, k4 = idx >> 7;
-      rb[i] = *reinterpret_cast<const f32x4*>(a.w + (int64_t)(n0 + n) * a.K + k0 + 4 * k4);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int idx = t + 256 * i;
-      const int p = idx & 31, k4 = (idx >> 5) & 3, b = idx >> 7;
-      if (b < R)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) As[buf][(4 * k4 + e) * AS + b * 32 + p] = ra[i][e];
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int idx = t + 256 * i;
-      const int n = idx & 127, k4 = idx >> 7;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) Bs[buf][(4 * k4 + e) * BS + n] = rb[i][e];
-    }
-  };
-
-  f32x16 acc[R];
-#pragma unroll
-  for (int b = 0; b < R; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-  const int nchunks = a.K / LK;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  const int m = lane & 31, kh = lane >> 5, bn = 32 * w + m;
-  for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1;
-    const bool more = c + 1 < nchunks;
-    if (more) gload((c + 1) * LK);
-    float av[LK / 2][R], bv[LK / 2];
-#pragma unroll
-    for (int kk = 0; kk < LK / 2; ++kk) {
-      const int kr = 2 * kk + kh;
-#pragma unroll
-      for (int b = 0; b < R; ++b) av[kk][b] = As[buf][kr * AS + b * 32 + m];
-      bv[kk] = Bs[buf][kr * BS + bn];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < LK / 2; ++kk)
-#pragma unroll
-      for (int b = 0; b < R; ++b)
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk][b], bv[kk], acc[b], 0, 0, 0);
-    if (more) lstore(buf ^ 1);
-    __syncthreads();
-  }
-
-  // epilogue: lane (point row of register r, feature n)
-  const int n = n0 + bn;
-  const float bias = a.bias[n];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t p = p0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-    if (p >= a.M) continue;
-    const int64_t o = p * a.N + n;
-    float v0 = acc[0][r] + bias;
-    if (RES) v0 += a.res[o];
-    a.y[o] = v0;
-    if (!ACT) {
-#pragma unroll
-      for (int b = 1; b < R; ++b) a.y[b * plane_y + o] = acc[b][r];
-      continue;
-    }
-    const float s = tt_sig10(v0), ds = TT_SCALE * s * (1.f - s);
-    a.h[o] = tt_softplus10(v0);
-#pragma unroll
-    for (int k = 0; k < NDIR; ++k) {
-      const int64_t oJ = (1 + k) * plane_y + o, oL = (1 + NDIR + k) * plane_y + o;
-      float J = acc[1 + k][r], L = acc[1 + NDIR + k][r];
-      if (RES) {
-        J += a.res[oJ];
-        L += a.res[oL];
-      }
-      a.y[oJ] = J;
-      a.y[oL] = L;
-      a.h[oJ] = J * s;
-      a.h[oL] = J * J * ds + L * s;
-    }
-  }
-}
-
 thread_local char g_err[512] = "";
 
 // CU count of the current device, cached per device (queried on every GEMM otherwise).
@@ -728,32 +586,5 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
 }
 
 const char* pntf_tt_gemm_last_error(void) { return g_err; }
-
-int pntf_tt_linear_act(int ndir, const float* x, int64_t m, int k, const float* w, int n,
-                       const float* bias, const float* res, int act, float* y, float* h,
-                       hipStream_t stream) {
-  if ((ndir != 3 && ndir != 6) || m < 0 || k % 16 != 0 || k <= 0 || n % 128 != 0 || n <= 0 ||
-      (res && !act) || (m > 0 && (!x || !w || !bias || !y || (act && !h)))) {
-    snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: bad arguments");
-    return PNTF_ERR_ARG;
-  }
-  if (m == 0) return PNTF_OK;
-  LinArgs a{x, w, bias, res, y, h, m, n, k};
-  dim3 grid((unsigned)((m + 31) / 32), (unsigned)(n / 128)), block(256);
-#define PNTF_LIN(ND)                                                                         \
-  if (res) hipLaunchKernelGGL((tt_linear_act_kernel<ND, true, true>), grid, block, 0, stream, a); \
-  else if (act) hipLaunchKernelGGL((tt_linear_act_kernel<ND, true, false>), grid, block, 0,   \
-                                   stream, a);                                                \
-  else hipLaunchKernelGGL((tt_linear_act_kernel<ND, false, false>), grid, block, 0, stream, a);
-  if (ndir == 3) { PNTF_LIN(3) }
-  else { PNTF_LIN(6) }
-#undef PNTF_LIN
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: %s", hipGetErrorString(e));
-    return PNTF_ERR_HIP;
-  }
-  return PNTF_OK;
-}
 
 }  // extern "C"

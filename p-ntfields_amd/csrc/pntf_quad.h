@@ -114,37 +114,30 @@ struct QCx {
 template <int QR>
 struct QRing {
   f32x4 r[QR];
+  int off;   // byte offset of the next fragment to load (wave-uniform)
 };
-// Load stream fragment `frag` (wave-uniform) into ring slot `slot`.  The fragment index is
-// the layer's stream position plus a compile-time offset (qlayer), so each load costs one
-// scalar add for its offset, not a runtime wrap test per fragment.
-template <int QR>
-__device__ __forceinline__ void qfetch(QRing<QR>& ring, Rsrc W, int lane, int slot, int frag) {
+// Load the next stream fragment into ring slot `slot`: one scalar add per load.  Only the
+// stream's last layer (WRAP) can run past the end of the stream, whose prefetch wraps into the
+// next step's first layer; the wrap test costs two more scalar ops there alone.
+template <int NF, int QR, bool WRAP>
+__device__ __forceinline__ void qfetch(QRing<QR>& ring, Rsrc W, int lane, int slot) {
 #ifdef PNTF_QABL_NOLOAD   // diagnostics only (tests/diag timing ablations; wrong results)
   ring.r[slot] = ring.r[slot] * 1.0001f;
 #else
-  ring.r[slot] = bload(W, lane * 16, frag * 1024);
+  ring.r[slot] = bload(W, lane * 16, ring.off);
 #endif
+  ring.off += 1024;
+  if constexpr (WRAP) ring.off = ring.off == NF * 1024 ? 0 : ring.off;
 }
-
-// Stream position (in 1 KiB fragments of one wave's stream) of quad layer L.
-constexpr int qpos(int L) { return q_layer_off(L) / 256; }
 
 // One layer: G groups of 16 out rows; per group IN/16 fragments of 4 k steps x NC columns;
 // B operands read from `in` (IN features, row stride IN/4 + 4).  The layer's first fragment
-// is stream fragment `pos` and sits in ring slot S0; consuming in-layer fragment f refills its
-// slot with fragment pos + f + QR (mod NF only where WRAP: the stream's last layer, whose
-// prefetch runs into the next step's first layer).  epi(g, v[NC]) gets the compact sums of
-// group g.
+// sits in ring slot S0.  epi(g, v[NC]) gets the compact sums of group g.
 template <int NC, int IN, int NF, int G, int S0, int QR, bool SOLO, bool WRAP = false,
           class Epi>
 __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, const lds_f* in,
-                                       int pos, Epi&& epi) {
+                                       Epi&& epi) {
   constexpr int SP = IN / 4 + 4, NQ = IN / 16;
-  auto next_frag = [&](int f) {
-    const int i = pos + f + QR;
-    return WRAP ? (i >= NF ? i - NF : i) : i;
-  };
   // B operands kept in registers for all groups of the layer when they fit (64 VGPRs):
   // one LDS read per fragment instead of one per fragment and group
   constexpr bool KEEP = PNTF_QKEEPB && G > 1 && NC * NQ <= 16;
@@ -183,7 +176,7 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[c][e % QCH] = fmaf(a[e], b[c][e], acc[c][e % QCH]);
-      qfetch<QR>(ring, W, cx.lane, slot, next_frag(g * NQ + q));
+      qfetch<NF, QR, WRAP>(ring, W, cx.lane, slot);
     });
     float v[NC];
     // the compact value of lane l is row r0 + 4·og + kb (the MFMA path's layout): take it
@@ -228,7 +221,7 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[c][e % QCH] = mfma4(a[e], b[c][e], acc[c][e % QCH]);
-      qfetch<QR>(ring, W, cx.lane, slot, next_frag(g * NQ + q));
+      qfetch<NF, QR, WRAP>(ring, W, cx.lane, slot);
     });
     float v[NC];
 #pragma unroll
@@ -298,7 +291,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[0] (:227); compat: the out_backgrad quirk (:435-438) stores σ10(softplus(y))
-  qlayer<2, 256, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, F, qpos(0), [&](int g, const float (&v)[2]) {
+  qlayer<2, 256, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       SpSig q = sp_sig(v[c] + pick(aux[0], g));
@@ -311,7 +304,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int la = 1 + 2 * blk, sa = QS_EBLK + 8 * blk;
-    qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, qpos(la), [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         SpSig q = sp_sig(v[c] + pick(aux[la], g));
@@ -320,7 +313,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
       }
     });
     qsync();
-    qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, qpos(la + 1), [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -332,7 +325,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
     qsync();
   }
   // ---- encoder[-1] (:234) and the smooth max / min merge (:236-244): u = [M | m] -> B
-  qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, qpos(5), [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const float zs = v[0] + pick(aux[5], g), zg = v[1] + pick(aux[5], g);
     const float d = zs - zg;
     const float e = exp_neg10abs(d);
@@ -351,13 +344,13 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   for (int i = 0; i < 3; ++i) {
     const f32x4 ba = i == 0 ? aux[6] : i == 1 ? aux[8] : aux[10];
     const f32x4 bb = i == 0 ? aux[7] : i == 1 ? aux[9] : aux[11];
-    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, B, qpos(6) + i * (qpos(8) - qpos(6)), [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       SpSig q = sp_sig(v[0] + pick(ba, g));
       *cx.at<256>(A, 0, g) = q.sp;
       if (GRAD) *cx.sig(QS_GBLK + 8 * i + g) = q.sg;
     });
     qsync();
-    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, qpos(7) + i * (qpos(8) - qpos(6)), [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       SpSig q = sp_sig(v[0] + pick(bb, g) + *o);
       *o = q.sp;
@@ -367,7 +360,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   // ---- generator[-2] + act (:251-252) and the head generator[-1] (:254-255)
   float part[1] = {0.f};
-  qlayer<1, 256, NF, 2, 16 % QR, QR, SOLO, NF == Q_NF_FWD>(ring, W, cx, B, qpos(12), [&](int g, const float (&v)[1]) {
+  qlayer<1, 256, NF, 2, 16 % QR, QR, SOLO, NF == Q_NF_FWD>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
     SpSig q = sp_sig(v[0] + pick(aux[12], g));
     part[0] = fmaf(pick(aux[13], g), q.sp, part[0]);
     if (GRAD) *cx.sig(QS_G3 + g) = q.sg;
@@ -391,19 +384,19 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   for (int g = 0; g < 2; ++g) *cx.at<128>(A, 0, g) = dd * pick(aux[13], g) * *cx.sig(QS_G3 + g);
   qsync();
   // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> B
-  qlayer<1, 128, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, qpos(13), [&](int g, const float (&v)[1]) {
+  qlayer<1, 128, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
     *cx.at<256>(B, 0, g) = v[0] * *cx.sig(QS_GBLK + 16 + 4 + g);
   });
   qsync();
   // ---- generator blocks, reverse (:615-618): lb: B -> A, la: A (+ B residual) -> B
 #pragma unroll 1
   for (int i = 2; i >= 0; --i) {
-    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, B, qpos(14) + (2 - i) * (qpos(16) - qpos(14)), [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * i + g);
     });
     qsync();
     const int sb = QS_GBLK + 8 * (i - 1) + 4;   // σ10(y2) of block i - 1 (none for i = 0)
-    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, qpos(15) + (2 - i) * (qpos(16) - qpos(14)), [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       const float y = v[0] + *o;
       *o = i > 0 ? y * *cx.sig(sb + g) : y;
@@ -421,7 +414,7 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1): F -> A
-  qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, F, qpos(20), [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) *cx.at<128>(A, c, g) = v[c] * *cx.sig(QS_EBLK + 12 + 2 * g + c);
   });
@@ -431,12 +424,12 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
 #pragma unroll
   for (int blk = 1; blk >= 0; --blk) {
     const int sa = QS_EBLK + 8 * blk, sbelow = blk ? QS_EBLK + 4 : QS_E0;
-    qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, qpos(21 + 2 * (1 - blk)), [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) *cx.at<128>(B, c, g) = v[c] * *cx.sig(sa + 2 * g + c);
     });
     qsync();
-    qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, qpos(22 + 2 * (1 - blk)), [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -450,7 +443,7 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   float acc[2 * DIM];
 #pragma unroll
   for (int i = 0; i < 2 * DIM; ++i) acc[i] = 0.f;
-  qlayer<2, 128, NF, 4, 0 % QR, QR, SOLO, true>(ring, W, cx, A, qpos(25), [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, 4, 0 % QR, QR, SOLO, true>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const int f = cx.w * 64 + 16 * g + 4 * cx.og + cx.kb;
     const int fb = f & 127;
     float bw[DIM];
@@ -518,8 +511,9 @@ __global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
   for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
   aux[13][2] = a.P[OFF_BIAS + B_G4B];
   QRing<QR> ring;
+  ring.off = 0;
 #pragma unroll
-  for (int s = 0; s < QR; ++s) qfetch<QR>(ring, W, cx.lane, s, s);
+  for (int s = 0; s < QR; ++s) qfetch<NF, QR, false>(ring, W, cx.lane, s);
   const int64_t ntiles = (a.n + QPAIRS - 1) / QPAIRS;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t pair = tile * QPAIRS + (cx.lane & 3);
@@ -573,8 +567,9 @@ __global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
   for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
   aux[13][2] = a.P[OFF_BIAS + B_G4B];
   QRing<QRING> ring;
+  ring.off = 0;
 #pragma unroll
-  for (int s = 0; s < QRING; ++s) qfetch<QRING>(ring, W, cx.lane, s, s);
+  for (int s = 0; s < QRING; ++s) qfetch<Q_NF_ALL, QRING, false>(ring, W, cx.lane, s);
   const int cap = a.max_iter + 1;
   const int64_t rows = (int64_t)cap + 1;
   constexpr int TQ = SOLO ? 1 : QPAIRS;   // queries per tile

@@ -5,10 +5,16 @@
 //
 // Design ("Taylor tape"): the Taylor-mode forward of NN.out_laplace (:710-848)
 // is run layer by layer and every pre-activation is kept in HBM, then the reverse sweep
-// walks the tape back.  A Taylor tensor of M points and width W is stored as R = 1 + 2·ndir
-// planes (R, M, W): [value | ndir first-derivative rows | ndir diagonal second-derivative
-// rows] (ndir = dim in the encoder, 2·dim after the start/goal merge).  With that layout every
-// Linear of the graph is ONE plain fp32 GEMM over R·M rows (hipBLASLt, issued by the host),
+// walks the tape back.  The loss only needs each endpoint's Laplacian Δ_eτ = Σ_{d∈e} ∂²τ/∂x_d²
+// (Model.Loss :919-920), and the diagonal second-derivative rows enter every layer linearly
+// (Linear: L' = A L; act: L' = σ'J² + σL; merge: L_M = s0 L + c J², ...), so the tape carries
+// their SUM per endpoint instead of one row per direction: a Taylor tensor of M points and
+// width W is R = 1 + ndir + nl planes (R, M, W) = [value | ndir first-derivative rows | nl
+// summed second-derivative rows], (ndir, nl) = (dim, 1) in the encoder and (2·dim, 2) after the
+// start/goal merge ([∂x_start (dim) | ∂x_goal (dim) | Σ∂²x_start | Σ∂²x_goal]).  The loss
+// and its gradient are those of the reference's per-direction rows (the sums commute with
+// every operation); the Linear layers do 9 instead of 13 row GEMMs per pair (dim 3).  With
+// that layout every Linear of the graph is ONE plain fp32 GEMM over R·M rows (pntf_gemm.hip),
 // the bias touching plane 0 only, and everything between the GEMMs is a fused elementwise
 // kernel here — one HBM pass per layer where the reference issues ~10 torch ops:
 //   tt_fourier_kernel   input_mapping_laplace (:199-213)           Φ planes
@@ -63,7 +69,8 @@ __device__ __forceinline__ float softplus10(float y) {
 }
 
 // ---------------------------------------------------------------- Φ planes (:199-213)
-// phi (1 + 2 DIM, 2n, 256): point m < n is x_start of pair m, m >= n the x_goal of pair m - n.
+// phi (2 + DIM, 2n, 256): point m < n is x_start of pair m, m >= n the x_goal of pair m - n;
+// planes [value | ∂x_d (DIM) | Σ_d ∂²x_d].
 template <int DIM>
 __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict__ xp, int64_t n,
                                   const float* __restrict__ Btab, const int32_t* __restrict__ env,
@@ -78,15 +85,16 @@ __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict
     const int e = env ? env[p] : 0;
     float* o = phi + m * 256 + j;
     if (e < 0 || e >= n_env) {
-      for (int r = 0; r < 1 + 2 * DIM; ++r) o[r * plane] = o[r * plane + H] = NAN;
+      for (int r = 0; r < 2 + DIM; ++r) o[r * plane] = o[r * plane + H] = NAN;
       continue;
     }
     const float* B = Btab + (int64_t)e * DIM * H + j;
-    float w[DIM], q = 0.f;
+    float w[DIM], q = 0.f, w2 = 0.f;
 #pragma unroll
     for (int k = 0; k < DIM; ++k) {
       w[k] = TWO_PI * B[k * H];
       q = fmaf(x[k], w[k], q);
+      w2 = fmaf(w[k], w[k], w2);
     }
     float s, c;
     sincosf(q, &s, &c);
@@ -96,9 +104,9 @@ __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict
     for (int k = 0; k < DIM; ++k) {
       o[(1 + k) * plane] = w[k] * c;
       o[(1 + k) * plane + H] = -w[k] * s;
-      o[(1 + DIM + k) * plane] = -w[k] * w[k] * s;
-      o[(1 + DIM + k) * plane + H] = -w[k] * w[k] * c;
     }
+    o[(1 + DIM) * plane] = -w2 * s;
+    o[(1 + DIM) * plane + H] = -w2 * c;
   }
 }
 
@@ -110,14 +118,16 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
-// y (R, M, W): GEMM output; plane 0 gets the bias (kept in place as the saved
-// pre-activation).  ACT: h = softplus10(y), J' = σJ, L' = σ'J² + σL (σ = σ(10y), σ' = 10σ(1-σ)).
-// RES: the residual branch (:744, :828) res (R, M, W) is added to every plane first (and
-// the sum kept in y).
-template <int NDIR, bool ACT, bool RES>
+// y (R, M, W), R = 1 + NDIR + NL: GEMM output; plane 0 gets the bias (kept in place as the
+// saved pre-activation).  ACT: h = softplus10(y), J' = σJ, L'_l = σ' Σ_{k∈l} J_k² + σ L_l
+// (σ = σ(10y), σ' = 10σ(1-σ); summed row l covers the J rows k of its endpoint group,
+// l·NDIR/NL <= k < (l+1)·NDIR/NL).  RES: the residual branch (:744, :828) res (R, M, W) is
+// added to every plane first (and the sum kept in y).
+template <int NDIR, int NL, bool ACT, bool RES>
 __global__ __launch_bounds__(256) void tt_act_fwd_kernel(float* __restrict__ y, float* __restrict__ h,
                                   const float* __restrict__ bias, const float* __restrict__ res,
                                   int64_t M, int W) {
+  constexpr int GK = NDIR / NL;
   const int64_t plane = M * W;
   for (int64_t i = 4 * (blockIdx.x * (int64_t)blockDim.x + threadIdx.x); i < plane;
        i += 4 * (int64_t)gridDim.x * blockDim.x) {
@@ -134,17 +144,26 @@ __global__ __launch_bounds__(256) void tt_act_fwd_kernel(float* __restrict__ y, 
     }
     st4(h + i, hv);
 #pragma unroll
-    for (int k = 0; k < NDIR; ++k) {
-      const int64_t iJ = (1 + k) * plane + i, iL = (1 + NDIR + k) * plane + i;
-      f4 J = ld4(y + iJ), L = ld4(y + iL);
+    for (int l = 0; l < NL; ++l) {
+      f4 jj = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = l * GK; k < (l + 1) * GK; ++k) {
+        const int64_t iJ = (1 + k) * plane + i;
+        f4 J = ld4(y + iJ);
+        if (RES) {
+          J += ld4(res + iJ);
+          st4(y + iJ, J);
+        }
+        st4(h + iJ, J * s);
+        jj += J * J;
+      }
+      const int64_t iL = (1 + NDIR + l) * plane + i;
+      f4 L = ld4(y + iL);
       if (RES) {
-        J += ld4(res + iJ);
         L += ld4(res + iL);
-        st4(y + iJ, J);
         st4(y + iL, L);
       }
-      st4(h + iJ, J * s);
-      st4(h + iL, J * J * ds + L * s);
+      st4(h + iL, jj * ds + L * s);
     }
   }
 }
@@ -167,14 +186,14 @@ __device__ __forceinline__ void block_colsum(f4 acc, float* __restrict__ partial
 }
 
 // Adjoint of act_laplace, in place on g (dL/dh planes in, dL/dy planes out):
-//   g_y = g_h σ + Σ_k g_Jk J_k σ' + g_Lk (J_k² σ'' + L_k σ')    σ'' = 10 σ' (1 - 2σ)
-//   g_J = g_J σ + 2 g_L J σ'      g_L = g_L σ
+//   g_y = g_h σ + Σ_k g_Jk J_k σ' + Σ_l g_Ll (σ'' Σ_{k∈l} J_k² + L_l σ')   σ'' = 10 σ' (1 - 2σ)
+//   g_Jk = g_Jk σ + 2 g_L(k) J_k σ'      g_Ll = g_Ll σ
 // ACT=false (a Linear with no activation) only forms the bias partials.
-template <int NDIR, int W, bool ACT>
+template <int NDIR, int NL, int W, bool ACT>
 __global__ __launch_bounds__(256) void tt_act_bwd_kernel(const float* __restrict__ y,
                                                          float* __restrict__ g, int64_t M,
                                                          float* __restrict__ partial) {
-  constexpr int TPR = W / 4, RB = 256 / TPR;
+  constexpr int TPR = W / 4, RB = 256 / TPR, GK = NDIR / NL;
   const int64_t plane = M * W;
   const int j = 4 * (threadIdx.x % TPR);
   f4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -194,11 +213,19 @@ __global__ __launch_bounds__(256) void tt_act_bwd_kernel(const float* __restrict
     }
     f4 gy = ld4(g + i) * s;
 #pragma unroll
-    for (int k = 0; k < NDIR; ++k) {
-      const int64_t iJ = (1 + k) * plane + i, iL = (1 + NDIR + k) * plane + i;
-      const f4 J = ld4(y + iJ), L = ld4(y + iL), gJ = ld4(g + iJ), gL = ld4(g + iL);
-      gy += gJ * J * ds + gL * (J * J * dds + L * ds);
-      st4(g + iJ, gJ * s + 2.f * gL * J * ds);
+    for (int l = 0; l < NL; ++l) {
+      const int64_t iL = (1 + NDIR + l) * plane + i;
+      const f4 L = ld4(y + iL), gL = ld4(g + iL);
+      f4 jj = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = l * GK; k < (l + 1) * GK; ++k) {
+        const int64_t iJ = (1 + k) * plane + i;
+        const f4 J = ld4(y + iJ), gJ = ld4(g + iJ);
+        gy += gJ * J * ds;
+        jj += J * J;
+        st4(g + iJ, gJ * s + 2.f * gL * J * ds);
+      }
+      gy += gL * (jj * dds + L * ds);
       st4(g + iL, gL * s);
     }
     st4(g + i, gy);
@@ -242,8 +269,9 @@ void launch_reduce(const float* partial, int nb, int W, float* out, int accumula
 }
 
 // ---------------------------------------------------------------- start/goal merge (:761-811)
-// z (1 + 2 DIM, 2n, 128) encoder output planes -> u (1 + 4 DIM, n, 256) generator planes
-// [value | ∂xs (DIM) | ∂xg (DIM) | ∂²xs (DIM) | ∂²xg (DIM)], features [max-part | min-part].
+// z (2 + DIM, 2n, 128) encoder output planes [value | ∂ (DIM) | Σ∂²] -> u (3 + 2 DIM, n, 256)
+// generator planes [value | ∂xs (DIM) | ∂xg (DIM) | Σ∂²xs | Σ∂²xg], features
+// [max-part | min-part]; c = 10 s0 s1 is the merge curvature (:768-813).
 template <int DIM>
 __global__ __launch_bounds__(256) void tt_merge_fwd_kernel(const float* __restrict__ z, int64_t n,
                                     float* __restrict__ u) {
@@ -258,24 +286,27 @@ __global__ __launch_bounds__(256) void tt_merge_fwd_kernel(const float* __restri
     u[o] = fmaxf(zs, zg) + lse;
     u[o + H] = fminf(zs, zg) - lse;
     const float s0 = sig10(d), s1 = 1.f - s0, c = SCALE * s0 * s1;
+    float jjs = 0.f, jjg = 0.f;
 #pragma unroll
     for (int k = 0; k < DIM; ++k) {
       const float Js = z[(1 + k) * pz + is], Jg = z[(1 + k) * pz + ig];
-      const float Ls = z[(1 + DIM + k) * pz + is], Lg = z[(1 + DIM + k) * pz + ig];
       u[(1 + k) * pu + o] = Js * s0;
       u[(1 + k) * pu + o + H] = Js * s1;
       u[(1 + DIM + k) * pu + o] = Jg * s1;
       u[(1 + DIM + k) * pu + o + H] = Jg * s0;
-      const float cs = c * Js * Js, cg = c * Jg * Jg;
-      u[(1 + 2 * DIM + k) * pu + o] = cs + Ls * s0;
-      u[(1 + 2 * DIM + k) * pu + o + H] = -cs + Ls * s1;
-      u[(1 + 3 * DIM + k) * pu + o] = cg + Lg * s1;
-      u[(1 + 3 * DIM + k) * pu + o + H] = -cg + Lg * s0;
+      jjs = fmaf(Js, Js, jjs);
+      jjg = fmaf(Jg, Jg, jjg);
     }
+    const float Ls = z[(1 + DIM) * pz + is], Lg = z[(1 + DIM) * pz + ig];
+    const float cs = c * jjs, cg = c * jjg;
+    u[(1 + 2 * DIM) * pu + o] = cs + Ls * s0;
+    u[(1 + 2 * DIM) * pu + o + H] = -cs + Ls * s1;
+    u[(2 + 2 * DIM) * pu + o] = cg + Lg * s1;
+    u[(2 + 2 * DIM) * pu + o + H] = -cg + Lg * s0;
   }
 }
 
-// Adjoint of the merge: gu (1 + 4 DIM, n, 256) -> gz (1 + 2 DIM, 2n, 128).
+// Adjoint of the merge: gu (3 + 2 DIM, n, 256) -> gz (2 + DIM, 2n, 128).
 template <int DIM>
 __global__ __launch_bounds__(256) void tt_merge_bwd_kernel(const float* __restrict__ z, const float* __restrict__ gu,
                                     int64_t n, float* __restrict__ gz) {
@@ -287,25 +318,25 @@ __global__ __launch_bounds__(256) void tt_merge_bwd_kernel(const float* __restri
     const int64_t is = p * H + j, ig = (n + p) * H + j, o = p * 256 + j;
     const float d = z[is] - z[ig];
     const float s0 = sig10(d), s1 = 1.f - s0, c = SCALE * s0 * s1;
-    float g_s0 = 0.f, g_c = 0.f;
+    const float Ls = z[(1 + DIM) * pz + is], Lg = z[(1 + DIM) * pz + ig];
+    const float gLsM = gu[(1 + 2 * DIM) * pu + o], gLsm = gu[(1 + 2 * DIM) * pu + o + H];
+    const float gLgM = gu[(2 + 2 * DIM) * pu + o], gLgm = gu[(2 + 2 * DIM) * pu + o + H];
+    const float dLs = gLsM - gLsm, dLg = gLgM - gLgm;
+    float g_s0 = dLs * Ls - dLg * Lg, jjs = 0.f, jjg = 0.f;
 #pragma unroll
     for (int k = 0; k < DIM; ++k) {
       const float Js = z[(1 + k) * pz + is], Jg = z[(1 + k) * pz + ig];
-      const float Ls = z[(1 + DIM + k) * pz + is], Lg = z[(1 + DIM + k) * pz + ig];
       const float gJsM = gu[(1 + k) * pu + o], gJsm = gu[(1 + k) * pu + o + H];
       const float gJgM = gu[(1 + DIM + k) * pu + o], gJgm = gu[(1 + DIM + k) * pu + o + H];
-      const float gLsM = gu[(1 + 2 * DIM + k) * pu + o];
-      const float gLsm = gu[(1 + 2 * DIM + k) * pu + o + H];
-      const float gLgM = gu[(1 + 3 * DIM + k) * pu + o];
-      const float gLgm = gu[(1 + 3 * DIM + k) * pu + o + H];
-      const float dLs = gLsM - gLsm, dLg = gLgM - gLgm;
-      g_s0 += (gJsM - gJsm) * Js - (gJgM - gJgm) * Jg + dLs * Ls - dLg * Lg;
-      g_c += dLs * Js * Js + dLg * Jg * Jg;
+      g_s0 += (gJsM - gJsm) * Js - (gJgM - gJgm) * Jg;
+      jjs = fmaf(Js, Js, jjs);
+      jjg = fmaf(Jg, Jg, jjg);
       gz[(1 + k) * pz + is] = gJsM * s0 + gJsm * s1 + 2.f * c * Js * dLs;
       gz[(1 + k) * pz + ig] = gJgM * s1 + gJgm * s0 + 2.f * c * Jg * dLg;
-      gz[(1 + DIM + k) * pz + is] = gLsM * s0 + gLsm * s1;
-      gz[(1 + DIM + k) * pz + ig] = gLgM * s1 + gLgm * s0;
     }
+    gz[(1 + DIM) * pz + is] = gLsM * s0 + gLsm * s1;
+    gz[(1 + DIM) * pz + ig] = gLgM * s1 + gLgm * s0;
+    const float g_c = dLs * jjs + dLg * jjg;
     const float kk = (g_s0 + g_c * SCALE * (1.f - 2.f * s0)) * c;
     const float gM = gu[o], gm = gu[o + H];
     gz[is] = gM * s0 + gm * s1 + kk;
@@ -320,9 +351,11 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// One wave per pair.  v (R, n, 128) = generator[3]'s Taylor output, R = 1 + 4 DIM.
-// Forward: y_r = w4·v_r (+ b4 on r = 0); τ = σ(0.1 y), ∇τ, Δτ rows (actout_laplace :693-708);
-// diff (Model.Loss :914-946, ARM: models/model_res_sigmoid.py:888-933).  Backward of
+// One wave per pair.  v (R, n, 128) = generator[3]'s Taylor output, R = 3 + 2 DIM planes
+// [value | ∂xs (DIM) | ∂xg (DIM) | Σ∂²xs | Σ∂²xg].
+// Forward: y_r = w4·v_r (+ b4 on r = 0); τ = σ(0.1 y), ∇τ and the per-endpoint Laplacian
+// Δ_eτ = Σ_{k∈e} (J_k² τ'' + L_e τ') (actout_laplace :693-708, summed as Model.Loss :919-920
+// does); diff (Model.Loss :914-946, ARM: models/model_res_sigmoid.py:888-933).  Backward of
 // scale·Σ diff: g_r per row, written as gv_r = g_r w4 (the input gradient of generator[4])
 // and folded into per-block partials of g_w4 = Σ g_r v_r and g_b4 = Σ g_0.
 template <int DIM, bool ARM>
@@ -330,7 +363,7 @@ __global__ __launch_bounds__(256) void tt_head_loss_kernel(
     const float* __restrict__ v, const float* __restrict__ w4, const float* __restrict__ b4,
     const float* __restrict__ xp, const float* __restrict__ yobs, int64_t n, float gamma,
     float scale, float* __restrict__ diff, float* __restrict__ gv, float* __restrict__ partial) {
-  constexpr int R = 1 + 4 * DIM, ND = 2 * DIM;
+  constexpr int ND = 2 * DIM, R = 3 + ND;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t plane = n * H;
   const float wa = w4[lane], wb = w4[lane + 64], bias = b4[0];
@@ -346,12 +379,15 @@ __global__ __launch_bounds__(256) void tt_head_loss_kernel(
     const float t = 1.f / (1.f + expf(-0.1f * y));
     const float dt = 0.1f * t * (1.f - t), ddt = 0.1f * dt * (1.f - 2.f * t);
     const float dddt = 0.1f * (ddt * (1.f - 2.f * t) - 2.f * dt * dt);
-    float dtau[ND], ltau[ND];
+    float dtau[ND], lap[2];
 #pragma unroll
-    for (int k = 0; k < ND; ++k) {
-      const float J = yr[1 + k], L = yr[1 + ND + k];
-      dtau[k] = J * dt;
-      ltau[k] = fmaf(J * J, ddt, L * dt);
+    for (int k = 0; k < ND; ++k) dtau[k] = yr[1 + k] * dt;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float jj = 0.f;
+#pragma unroll
+      for (int k = 0; k < DIM; ++k) jj = fmaf(yr[1 + e * DIM + k], yr[1 + e * DIM + k], jj);
+      lap[e] = fmaf(jj, ddt, yr[1 + ND + e] * dt);
     }
     // ---- Model.Loss and its adjoint
     const float* x = xp + p * 2 * DIM;
@@ -365,16 +401,15 @@ __global__ __launch_bounds__(256) void tt_head_loss_kernel(
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const float sgn = e == 0 ? 1.f : -1.f;
-      float dd = 0.f, nn = 0.f, lap = 0.f;
+      float dd = 0.f, nn = 0.f;
 #pragma unroll
       for (int k = 0; k < DIM; ++k) {
         dd = fmaf(dtau[e * DIM + k], D[k], dd);
         nn = fmaf(dtau[e * DIM + k], dtau[e * DIM + k], nn);
-        lap += ltau[e * DIM + k];
       }
       const float S = T0 * nn + sgn * 2.f * t * dd + t * t;
       const float rS = sqrtf(S);
-      const float yp = 1.f / (rS / (t * t) + gamma * lap);
+      const float yp = 1.f / (rS / (t * t) + gamma * lap[e]);
       const float yo = yobs[p * 2 + e];
       float dfy;
       if (ARM) {
@@ -398,16 +433,18 @@ __global__ __launch_bounds__(256) void tt_head_loss_kernel(
     float g0 = gt * dt;
 #pragma unroll
     for (int k = 0; k < ND; ++k) {
-      const float J = yr[1 + k], L = yr[1 + ND + k], gL = gl[k / DIM];
-      g0 += gd[k] * J * ddt + gL * fmaf(J * J, dddt, L * ddt);
+      const float J = yr[1 + k];
+      g0 += gd[k] * J * ddt + gl[k / DIM] * J * J * dddt;
     }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) g0 += gl[e] * yr[1 + ND + e] * ddt;
     gb += g0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       float g;
       if (r == 0) g = g0;
       else if (r <= ND) g = gd[r - 1] * dt + 2.f * gl[(r - 1) / DIM] * yr[r] * ddt;
-      else g = gl[(r - 1 - ND) / DIM] * dt;
+      else g = gl[r - 1 - ND] * dt;
       const float* row = v + r * plane + p * H;
       float* grow = gv + r * plane + p * H;
       gwa = fmaf(g, row[lane], gwa);
@@ -416,7 +453,7 @@ __global__ __launch_bounds__(256) void tt_head_loss_kernel(
       grow[lane + 64] = g * wb;
     }
   }
-  // per-block partials: [gridDim][128] for g_w4, then [gridDim] for g_b4
+// per-block partials: [gridDim][128] for g_w4, then [gridDim] for g_b4
   __shared__ float red[4][129];
   red[wave][lane] = gwa;
   red[wave][lane + 64] = gwb;
@@ -479,46 +516,55 @@ int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, cons
   return check_launch("tt_fourier_kernel");
 }
 
-int pntf_tt_act_fwd(int ndir, float* y, float* h, const float* bias, const float* res,
+int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, const float* res,
                     int64_t m, int w, int act, hipStream_t stream) {
-  if ((ndir != 3 && ndir != 6 && ndir != 12) || m < 0 || (w != 128 && w != 256) ||
-      (m > 0 && (!y || !bias || (act && !h))) || (res && !act))
+  const bool shape = (nl == 1 && (ndir == 3 || ndir == 6)) || (nl == 2 && (ndir == 6 || ndir == 12));
+  if (!shape || m < 0 || (w != 128 && w != 256) || (m > 0 && (!y || !bias || (act && !h))) ||
+      (res && !act))
     return fail("pntf_tt_act_fwd: bad arguments");
   if (m == 0) return PNTF_OK;
   const dim3 g(grid_1d(m * w / 4)), b(256);
-#define PNTF_ACT_FWD(N)                                                                   \
-  if (res) hipLaunchKernelGGL((tt_act_fwd_kernel<N, true, true>), g, b, 0, stream, y, h, bias, \
-                              res, m, w);                                                 \
-  else if (act) hipLaunchKernelGGL((tt_act_fwd_kernel<N, true, false>), g, b, 0, stream, y, h, \
-                                   bias, res, m, w);                                      \
-  else hipLaunchKernelGGL((tt_act_fwd_kernel<N, false, false>), g, b, 0, stream, y, h, bias, \
+#define PNTF_ACT_FWD(N, L)                                                                  \
+  if (res) hipLaunchKernelGGL((tt_act_fwd_kernel<N, L, true, true>), g, b, 0, stream, y, h,   \
+                              bias, res, m, w);                                             \
+  else if (act) hipLaunchKernelGGL((tt_act_fwd_kernel<N, L, true, false>), g, b, 0, stream, y, \
+                                   h, bias, res, m, w);                                     \
+  else hipLaunchKernelGGL((tt_act_fwd_kernel<N, L, false, false>), g, b, 0, stream, y, h, bias, \
                           res, m, w);
-  if (ndir == 3) { PNTF_ACT_FWD(3) }
-  else if (ndir == 6) { PNTF_ACT_FWD(6) }
-  else { PNTF_ACT_FWD(12) }
+  if (nl == 1) {
+    if (ndir == 3) { PNTF_ACT_FWD(3, 1) }
+    else { PNTF_ACT_FWD(6, 1) }
+  } else {
+    if (ndir == 6) { PNTF_ACT_FWD(6, 2) }
+    else { PNTF_ACT_FWD(12, 2) }
+  }
 #undef PNTF_ACT_FWD
   return check_launch("tt_act_fwd_kernel");
 }
 
-int pntf_tt_act_bwd(int ndir, const float* y, float* g, int64_t m, int w, int act, float* gbias,
-                    int accumulate, float* partial, hipStream_t stream) {
-  if ((ndir != 3 && ndir != 6 && ndir != 12) || m < 0 || (w != 128 && w != 256) || !gbias ||
-      !partial || (m > 0 && (!g || (act && !y))))
+int pntf_tt_act_bwd(int ndir, int nl, const float* y, float* g, int64_t m, int w, int act,
+                    float* gbias, int accumulate, float* partial, hipStream_t stream) {
+  const bool shape = (nl == 1 && (ndir == 3 || ndir == 6)) || (nl == 2 && (ndir == 6 || ndir == 12));
+  if (!shape || m < 0 || (w != 128 && w != 256) || !gbias || !partial ||
+      (m > 0 && (!g || (act && !y))))
     return fail("pntf_tt_act_bwd: bad arguments");
   const int nb = nb_for(m / (1024 / w));
   const dim3 gr(nb), b(256);
-#define PNTF_ACT_BWD(N, W)                                                                 \
-  if (act) hipLaunchKernelGGL((tt_act_bwd_kernel<N, W, true>), gr, b, 0, stream, y, g, m,     \
+#define PNTF_ACT_BWD(N, L, W)                                                              \
+  if (act) hipLaunchKernelGGL((tt_act_bwd_kernel<N, L, W, true>), gr, b, 0, stream, y, g, m,  \
                               partial);                                                     \
-  else hipLaunchKernelGGL((tt_act_bwd_kernel<N, W, false>), gr, b, 0, stream, y, g, m, partial);
-  if (w == 128) {
-    if (ndir == 3) { PNTF_ACT_BWD(3, 128) }
-    else if (ndir == 6) { PNTF_ACT_BWD(6, 128) }
-    else { PNTF_ACT_BWD(12, 128) }
+  else hipLaunchKernelGGL((tt_act_bwd_kernel<N, L, W, false>), gr, b, 0, stream, y, g, m, \
+                          partial);
+  if (nl == 1) {   // encoder planes are 128 wide
+    if (w != 128) return fail("pntf_tt_act_bwd: encoder planes are 128 wide");
+    if (ndir == 3) { PNTF_ACT_BWD(3, 1, 128) }
+    else { PNTF_ACT_BWD(6, 1, 128) }
+  } else if (w == 128) {
+    if (ndir == 6) { PNTF_ACT_BWD(6, 2, 128) }
+    else { PNTF_ACT_BWD(12, 2, 128) }
   } else {
-    if (ndir == 3) { PNTF_ACT_BWD(3, 256) }
-    else if (ndir == 6) { PNTF_ACT_BWD(6, 256) }
-    else { PNTF_ACT_BWD(12, 256) }
+    if (ndir == 6) { PNTF_ACT_BWD(6, 2, 256) }
+    else { PNTF_ACT_BWD(12, 2, 256) }
   }
 #undef PNTF_ACT_BWD
   launch_reduce(partial, nb, w, gbias, accumulate, stream);

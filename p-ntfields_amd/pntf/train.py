@@ -17,8 +17,11 @@ Taylor-mode graph `NN.out_laplace` (:710-848) with autograd; here the adjoint is
            (+ the residual branch, accumulated in place by the GEMM) → merge adjoint
            (tt_merge_bwd)
 
-Layout: a Taylor tensor of M points and width W is (R, M, W) fp32, R = 1 + 2·ndir planes
-[value | ∂ (ndir) | diagonal ∂² (ndir)], ndir = dim in the encoder and 2·dim after the merge.
+Layout: a Taylor tensor of M points and width W is (R, M, W) fp32, R = 1 + ndir + nl planes
+[value | ∂ (ndir) | Σ diagonal ∂² (nl)], (ndir, nl) = (dim, 1) in the encoder and (2·dim, 2)
+after the merge: the loss needs each endpoint's Laplacian only (Model.Loss :919-920), and the
+reference's per-direction second-derivative rows enter every layer linearly, so the tape
+carries their per-endpoint sums (R = 5 / 9 instead of 7 / 13 rows per point for dim 3).
 The GEMMs are the library's own fp32 MFMA kernels (pntf_tt_gemm: v_mfma_f32_32x32x2_f32,
 128 x 128 LDS tiles, deterministic split-K for the weight gradients); every elementwise stage
 is a HIP kernel of libpntf.so (csrc/pntf_train.hip).  There is no CPU path and no vendor GEMM.
@@ -88,34 +91,29 @@ class _Tape:
     """Forward tape of one loss evaluation: (name, input planes, pre-activation planes, act,
     has_residual) per Linear, in execution order."""
 
-    def __init__(self, params, dim, device, fused=False):
+    def __init__(self, params, dim, device):
         self.p = params
         self.dim = dim
         self.dev = device
-        self.fused = fused
         self.s = _stream(device)
         self.lib = _lib.load()
         self.ops = []
+
+    def planes(self, R):
+        """(ndir, nl) of a Taylor tensor with R planes: (dim, 1) in the encoder, (2dim, 2)
+        after the merge (pntf_train.hip)."""
+        return (self.dim, 1) if R == 2 + self.dim else (2 * self.dim, 2)
 
     def lin(self, x3, name, act=True, res=None):
         W, b = self.p[name + ".weight"], self.p[name + ".bias"]
         R, M, K = x3.shape
         N = W.shape[0]
-        ndir = (R - 1) // 2
+        ndir, nl = self.planes(R)
         y = torch.empty((R, M, N), dtype=torch.float32, device=self.dev)
         h = torch.empty_like(y) if act else None
-        if self.fused and ndir in (3, 6):
-            # GEMM + bias/residual/act_laplace in one kernel (32 points x all planes per tile);
-            # off by default: it measured slower than the two passes (DESIGN.md §3)
-            st = self.lib.pntf_tt_linear_act(ndir, _vp(x3), M, K, _vp(W), N, _vp(b), _vp(res),
-                                             int(act), _vp(y), _vp(h), self.s)
-            if st != 0:
-                raise PntfError("pntf_tt_linear_act: " +
-                                self.lib.pntf_tt_gemm_last_error().decode())
-        else:
-            gemm(y.view(R * M, N), x3.view(R * M, K), W, ta=False, tb=True)
-            check(self.lib.pntf_tt_act_fwd(ndir, _vp(y), _vp(h), _vp(b), _vp(res), M, N,
-                                           int(act), self.s), "pntf_tt_act_fwd")
+        gemm(y.view(R * M, N), x3.view(R * M, K), W, ta=False, tb=True)
+        check(self.lib.pntf_tt_act_fwd(ndir, nl, _vp(y), _vp(h), _vp(b), _vp(res), M, N,
+                                       int(act), self.s), "pntf_tt_act_fwd")
         self.ops.append((name, x3, y, act, res is not None))
         return h if act else y
 
@@ -127,7 +125,7 @@ def weight_grad(g2, x2, out):
     gemm(out, g2, x2, ta=True, tb=False)
 
 
-def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads, fused=False):
+def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
     """diff (n,) of Model.Loss and, into `grads` (key -> tensor shaped like the parameter),
     the gradient of scale·Σ diff w.r.t. every trained parameter.
 
@@ -140,9 +138,9 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads, fused=
         for g in grads.values():
             g.zero_()
         return torch.empty(0, dtype=torch.float32, device=dev)
-    tape = _Tape(params, dim, dev, fused)
+    tape = _Tape(params, dim, dev)
     s = tape.s
-    Re, Rg = 1 + 2 * dim, 1 + 4 * dim
+    Re, Rg = 2 + dim, 3 + 2 * dim        # summed second-derivative planes (pntf_train.hip)
     phi = torch.empty((Re, 2 * n, 2 * H), dtype=torch.float32, device=dev)
     n_env = Btab.shape[0]
     check(lib.pntf_tt_fourier(dim, _vp(xp), n, _vp(Btab), _vp(env), n_env, _vp(phi), s),
@@ -170,7 +168,8 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads, fused=
     for name, x3, y, act, has_res in reversed(tape.ops):
         R, M, K = x3.shape
         N = y.shape[2]
-        check(lib.pntf_tt_act_bwd((R - 1) // 2, _vp(y), _vp(g), M, N, int(act),
+        ndir, nl = tape.planes(R)
+        check(lib.pntf_tt_act_bwd(ndir, nl, _vp(y), _vp(g), M, N, int(act),
                                   _vp(grads[name + ".bias"]), 0, _vp(part), s),
               "pntf_tt_act_bwd")
         g2 = g.view(R * M, N)

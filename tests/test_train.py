@@ -439,33 +439,6 @@ def test_training_uses_no_vendor_gemm():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dim,n", [(3, 1), (3, 333), (6, 77)])
-def test_fused_linear_act_matches_two_pass(dim, n):
-    """pntf_tt_linear_act (GEMM + bias/residual/act_laplace in one kernel, 32 points x all
-    planes per tile) gives the same loss and weight gradients as pntf_tt_gemm followed by
-    pntf_tt_act_fwd; ragged point counts (tile edges), both Taylor widths (R = 7, 13)."""
-    from pntf import train
-    dev = torch.device("cuda:0")
-    W = weights() if dim == 3 else synth.make_weights(3)
-    xp = synth.make_pairs(n, dim, seed=50 + n)
-    yobs = synth.make_speeds(n, seed=51 + n)
-    Bt = synth.make_B_table(2, dim, first_seed=7)
-    env = synth.make_env_ids(n, 2, contiguous=False, seed=n)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
-    params = {k: torch.from_numpy(W[k]).to(dev) for k in train.trained_keys()}
-    out = []
-    for fused in (True, False):
-        grads = {k: torch.empty_like(v) for k, v in params.items()}
-        diff = train.loss_grad(params, T(xp), T(yobs), T(Bt), T(env), dim, 1e-3, 1.0 / n,
-                               dim == 6, grads, fused=fused)
-        out.append((diff.cpu().numpy(), {k: g.cpu().numpy() for k, g in grads.items()}))
-    (d1, g1), (d2, g2) = out
-    assert _rel(d1, d2) < 1e-5
-    for k in g1:
-        assert _rel(g1[k], g2[k]) < 1e-5, k
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["misaligned", "beta_half", "narrow_k"])
 def test_panel_gemm_fallbacks_vs_fp64(case):
     """Shapes / operands the register-panel kernel does not take fall back to the LDS-tiled

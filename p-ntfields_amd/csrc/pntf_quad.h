@@ -117,17 +117,18 @@ struct QRing {
   int off;   // byte offset of the next fragment to load (wave-uniform)
 };
 // Load the next stream fragment into ring slot `slot`: one scalar add per load.  Only the
-// stream's last layer (WRAP) can run past the end of the stream, whose prefetch wraps into the
-// next step's first layer; the wrap test costs two more scalar ops there alone.
+// stream's last layer (WRAP) prefetches past the end of the stream, into the next step's first
+// layer: there the offset is wrapped before the load (two more scalar ops, that layer alone;
+// the layer before it leaves the offset at the end of the stream).
 template <int NF, int QR, bool WRAP>
 __device__ __forceinline__ void qfetch(QRing<QR>& ring, Rsrc W, int lane, int slot) {
+  if constexpr (WRAP) ring.off = ring.off == NF * 1024 ? 0 : ring.off;
 #ifdef PNTF_QABL_NOLOAD   // diagnostics only (tests/diag timing ablations; wrong results)
   ring.r[slot] = ring.r[slot] * 1.0001f;
 #else
   ring.r[slot] = bload(W, lane * 16, ring.off);
 #endif
   ring.off += 1024;
-  if constexpr (WRAP) ring.off = ring.off == NF * 1024 ? 0 : ring.off;
 }
 
 // One layer: G groups of 16 out rows; per group IN/16 fragments of 4 k steps x NC columns;

@@ -282,6 +282,12 @@ __device__ __forceinline__ void store_tile(Scratch sc, int tile, int lane, f32x4
   __builtin_amdgcn_raw_buffer_store_b128(
       __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), sc.r, lane * 16,
       tile * 1024, AUX_NT);
+#if defined(PNTF_DIAG_WAITS) && (PNTF_DIAG_WAITS >> 6) & 1   // diagnostics only
+  asm volatile("s_waitcnt expcnt(0)" ::: "memory");
+#endif
+#if defined(PNTF_DIAG_WAITS) && (PNTF_DIAG_WAITS >> 7) & 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
 __device__ __forceinline__ f32x4 load_tile(Scratch sc, int tile, int lane) {
 #ifdef PNTF_ABL_NOLOAD    // diagnostics only (tests/diag ablations)

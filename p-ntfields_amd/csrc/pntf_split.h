@@ -60,6 +60,14 @@ __device__ float* pntf_dbg;
 typedef __attribute__((address_space(3))) float lds_f;
 typedef __attribute__((address_space(3))) f32x4 lds_f4;
 
+// Diagnostics only (DESIGN.md §7.5 bisection, tests/diag): -DPNTF_DIAG_WAITS=<bit mask> puts a
+// full s_waitcnt at the marked points of the split kernels.
+#ifndef PNTF_DIAG_WAITS
+#define PNTF_DIAG_WAITS 0
+#endif
+#define PNTF_DIAG_WAIT(bit)                                                                  \
+  if constexpr ((PNTF_DIAG_WAITS >> (bit)) & 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
 // Every wave's LDS writes done, then the workgroup barrier.  Written as one asm block with
 // a memory clobber: the s_barrier builtin alone is not a compiler barrier for LDS accesses.
 __device__ __forceinline__ void wg_sync() {
@@ -83,6 +91,7 @@ template <int OTL, int NC>
 __device__ __forceinline__ void exchange(const Split& sp, int buf, const f32x4 (&L)[16],
                                          f32x4 (&X)[16]) {
   constexpr int OTG = OTL * SPLIT;
+  PNTF_DIAG_WAIT(0)
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
@@ -94,7 +103,13 @@ __device__ __forceinline__ void exchange(const Split& sp, int buf, const f32x4 (
     }
   wg_sync();
 #pragma unroll
-  for (int i = 0; i < NC * OTG; ++i) X[i] = *sp.tile(buf, i);
+  for (int i = 0; i < NC * OTG; ++i) {
+    X[i] = *sp.tile(buf, i);
+    if constexpr ((PNTF_DIAG_WAITS >> 5) & 1) {   // at most 8 LDS reads in flight
+      if (i == 7) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  PNTF_DIAG_WAIT(1)
 #ifdef PNTF_DIAG_EXNOP
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 7" ::: "memory");
 #endif
@@ -124,6 +139,7 @@ __device__ __forceinline__ void slice(const f32x4 (&X)[16], int w, f32x4 (&R)[16
 // Sum of one value per lane over the 4 waves, in wave order (identical in every wave).
 template <int NV>
 __device__ __forceinline__ void reduce_waves(const Split& sp, float (&v)[NV]) {
+  PNTF_DIAG_WAIT(8)
 #pragma unroll
   for (int j = 0; j < NV; ++j) *sp.red(sp.w, j) = v[j];
   wg_sync();
@@ -377,6 +393,7 @@ __device__ __forceinline__ void split_backward(Ring& ring, const float* __restri
 
   // ---- head and generator[-2] (:592-613): dv = d · G4 ⊙ σ10(y3), local tiles -> X[0..7]
   const float dd = 0.1f * tau * (1.f - tau);
+  PNTF_DIAG_WAIT(2)
 #pragma unroll
   for (int t = 0; t < G3OTL; ++t) L[t] = (dd * cy.g4w[t]) * cy.sg3[t];
   exchange<G3OTL, 1>(sp, 0, L, X);
@@ -428,6 +445,7 @@ __device__ __forceinline__ void split_backward(Ring& ring, const float* __restri
     X[t] = s0 * dM + s1 * dm;
     X[8 + t] = s1 * dM + s0 * dm;
   }
+  PNTF_DIAG_WAIT(3)
 #ifdef PNTF_DIAG_MERGENOP   // diagnostics only (tests/diag split variants)
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #endif
@@ -438,6 +456,7 @@ __device__ __forceinline__ void split_backward(Ring& ring, const float* __restri
     layer<EOTL, 8, 2, 2, SITE_BWD_ENC, 2>(ring, W, Bk + OFF_E3 * 4 + wofs<8, 8>(w), X, lane, e3,
                                            NoPre{}, Head<8, 2>{WE + 3 * SZ_E * 4});
     flush(e3);
+    PNTF_DIAG_WAIT(4)
 #ifdef PNTF_DEBUG_DUMP
     for (int i_ = 0; i_ < 2 * EOTL; ++i_) { PNTF_DUMPW(40, i_, L[i_]) }
 #endif

@@ -151,11 +151,17 @@ int pntf_plan(const float* packed, int dim, const float* xp0, int64_t q, const f
               hipStream_t stream);
 
 /* pntf_plan with an explicit schedule (pntf_plan uses PNTF_SCHED_AUTO):
- *   PNTF_SCHED_WAVE_TILE   one wave per 16-query tile (throughput: many queries);
+ *   PNTF_SCHED_WAVE_TILE   one wave per 16-query tile (throughput: many queries; WIDE_TILE
+ *                          is treated as WAVE_TILE);
  *   PNTF_SCHED_SPLIT_TILE  the 4 waves of a workgroup share a tile, each computing a quarter
- *                          of every layer's outputs (latency: few queries, down to q = 1);
- *   PNTF_SCHED_AUTO        split while ceil(q/16) <= 2 x the device's CU count.
- * Results agree between schedules to fp32 rounding (the cross-wave sums are reordered). */
+ *                          of every layer's outputs;
+ *   PNTF_SCHED_QUAD_TILE   the 4 waves of a workgroup share a 4-query tile (no workspace);
+ *   PNTF_SCHED_AUTO        quad while ceil(q/4) <= the CU count — q <= CUs on the SOLO VALU
+ *                          layers, larger batches with the tail hand-off when ws holds
+ *                          8 + 8q bytes — split while ceil(q/16) <= 2 x the CU count, wave above.
+ * Results agree between schedules to fp32 rounding (the cross-wave sums are reordered);
+ * SOLO and the quad MFMA layers agree bit for bit.  WAVE/SPLIT need `ws`
+ * (pntf_workspace_bytes(q)). */
 int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, const float* Btab,
                  const int32_t* env, int32_t n_env, int mode, float step, float tol,
                  int32_t max_iter, float* path, int32_t* steps, void* ws, size_t ws_bytes,

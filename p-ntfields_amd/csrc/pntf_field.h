@@ -126,6 +126,19 @@ __device__ __forceinline__ Rsrc make_rsrc(const float* p, int bytes) {
 __device__ __forceinline__ f32x4 bload(Rsrc r, int voff, int soff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
+// 16-byte buffer store.  On gfx950 an instruction that overwrites a 16-byte store's data VGPRs
+// right after it corrupts the stored values in lanes 12-15 of every 16-lane row, and LLVM's
+// hazard recognizer skips the wait state that needs for buffer stores with an SGPR soffset
+// (DESIGN.md §7.5).  The s_nop reads the data, so nothing overwrites it before one wait state
+// has passed; pntf/build.py's store-data guard checks every kernel's assembly.
+template <int AUX>
+__device__ __forceinline__ void bstore(Rsrc r, f32x4 v, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(
+      __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, voff, soff, AUX);
+#ifndef PNTF_BSTORE_UNGUARDED   // test only: tests/test_capi_host.py checks the guard fires
+  asm volatile("s_nop 0" ::"v"(v));
+#endif
+}
 
 // Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).  Guarantees full
 // unrolling (constant register-array indices) however long the layer's step sequence is.
@@ -279,9 +292,7 @@ __device__ __forceinline__ void store_tile(Scratch sc, int tile, int lane, f32x4
 #ifdef PNTF_DIAG_STORENOP  // diagnostics only (tests/diag split variants)
   asm volatile("s_nop 7\n\ts_nop 7" ::"v"(v));
 #endif
-  __builtin_amdgcn_raw_buffer_store_b128(
-      __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), sc.r, lane * 16,
-      tile * 1024, AUX_NT);
+  bstore<AUX_NT>(sc.r, v, lane * 16, tile * 1024);
 #if defined(PNTF_DIAG_WAITS) && (PNTF_DIAG_WAITS >> 6) & 1   // diagnostics only
   asm volatile("s_waitcnt expcnt(0)" ::: "memory");
 #endif

@@ -345,6 +345,7 @@ __device__ __forceinline__ f32x4 pg_load(Rsrc r, int voff, int soff) {
 __device__ __forceinline__ void pg_store(Rsrc r, f32x4 v, int voff, int soff) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
                                          r, voff, soff, 0);
+  asm volatile("s_nop 0" ::"v"(v));   // store-data hazard guard (pntf_field.h bstore)
 }
 
 template <int KC, int NC, bool ACC>

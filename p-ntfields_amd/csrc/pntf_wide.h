@@ -54,9 +54,7 @@ __device__ __forceinline__ void wstore(WScratch sc, int t, int lane, const f32x1
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     f32x4 p{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
-    __builtin_amdgcn_raw_buffer_store_b128(
-        __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, p), sc.r, lane * 16,
-        t * 4096 + q * 1024, AUX_NT);
+    bstore<AUX_NT>(sc.r, p, lane * 16, t * 4096 + q * 1024);
   }
 }
 __device__ __forceinline__ f32x16 wload(WScratch sc, int t, int lane) {

@@ -17,7 +17,11 @@ Codegen guards fail the build instead of shipping a wrong kernel:
     that reads the result of a transcendental (v_exp/v_log/v_rcp/v_sin/v_cos) issued a few
     instructions earlier sees stale values in lanes 12-15 of every 16-lane row; ROCm 7.2's
     hazard recognizer under-pads that pair (measured: tests/diag).  Packed-fp32
-    codegen is therefore disabled for the device (-packed-fp32-ops), which costs nothing here.
+    codegen is therefore disabled for the device (-packed-fp32-ops), which costs nothing here;
+  * no vector store of more than 8 bytes whose data VGPRs the very next instruction overwrites
+    (store_data_hazards).  On gfx950 that overwrite corrupts the stored data in lanes 12-15 of
+    every 16-lane row; LLVM's hazard recognizer pads the pair except for MUBUF stores with an
+    SGPR soffset, so every buffer store passes soffset 0 (measured: tests/diag).
 A summary of every kernel's registers and spills is written to build/report.json.
 """
 import argparse
@@ -50,6 +54,41 @@ BUFFER_LOAD = re.compile(r"buffer_load_dwordx4 v\[\d+:\d+\], v\d+, (s\[\d+:\d+\]
 # units whose kernels keep a saved-σ scratch slot (τ-only / travel-time kernels have none)
 SCRATCH_UNITS = re.compile(r"^(field_d\d_k[123]|fsplit_d\d_k[123]|wide_d\d_k[123]|plan_d\d|plan_split_d\d|"
                            r"residual_d\d)$")
+
+
+WIDE_STORE = re.compile(r"^(buffer|global|scratch|flat)_store_dwordx[34]\b")
+
+
+def _vregs(tok):
+    m = re.match(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def store_data_hazards(asm):
+    """Store-data guard: (line, instruction) of every VALU instruction that
+    writes a data VGPR of a vector store of more than 8 bytes with no wait state between them (an
+    s_nop k gives k + 1).  Straight-line over the listing, so a store at the end of a block and
+    the first instruction of the next are also paired (conservative)."""
+    out, pend, meta = [], set(), False
+    for ln, line in enumerate(asm.splitlines(), 1):
+        s = line.strip()
+        meta = (meta or s.startswith(".amdgpu_metadata")) and \
+            not s.startswith(".end_amdgpu_metadata")
+        if meta or not s or s[0] in ";." or s.endswith(":") or line[:1] not in " \t":
+            continue
+        parts = s.split(";")[0].replace(",", " ").split()
+        op, ops = parts[0], parts[1:]
+        # VALU / MFMA writers only: a load's data returns hundreds of cycles after it issues
+        dst = _vregs(ops[0]) if op.startswith("v_") and ops else set()
+        if dst & pend:
+            out.append((ln, s))
+        pend = set()
+        if WIDE_STORE.match(op):      # MUBUF: vdata first; FLAT/global/scratch: vaddr, vdata
+            pend = _vregs(ops[0] if op.startswith("buffer") else ops[1])
+    return out
 
 
 def scratch_policy_violations(asm):
@@ -197,9 +236,13 @@ def _compile(unit, uid=None):
             raise RuntimeError("SGPR spills in %s (must stay spill-free): %s" % (name, sbad))
     for asm in glob.glob(os.path.join(d, "*amdgcn*gfx950*.s")):
         with open(asm) as fh:
-            m = PACKED_FP32.search(fh.read())
+            text = fh.read()
+        m = PACKED_FP32.search(text)
         if m:
             raise RuntimeError("packed-fp32 op %s in %s (hazard guard)" % (m.group(0), asm))
+        hz = store_data_hazards(text)
+        if hz:
+            raise RuntimeError("store-data hazard in %s (%d, first %s)" % (asm, len(hz), hz[0]))
         if SCRATCH_UNITS.match(name):
             with open(asm) as fh:
                 descs, good, bad = scratch_policy_violations(fh.read())

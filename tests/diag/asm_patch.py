@@ -9,6 +9,14 @@ POLICY: none | allmfma (STATES after every MFMA) | raw (non-MFMA reader of an MF
         result) | war (non-MFMA writer of a register an MFMA read; warv: VMEM loads excluded) | valu2mfma (MFMA reading a
         register a non-MFMA wrote) — each pads the instruction pair to at least STATES
         (default 24) wait states.  Counting is straight-line (labels do not reset it).
+        Waitcnt rewrites (DESIGN.md §7.5 bisection): vm0 / lgkm0 turn every compiler-emitted
+        partial vmcnt / lgkmcnt wait into a full one, exp0 adds expcnt(0) to every s_waitcnt.
+        After-class inserts: wz_<cls> puts a full s_waitcnt 0 after, nop_<cls> an s_nop 0 after,
+        every instruction of class cls = all | vload | vstore | lds | smem | valu | mfma (wz_all
+        restates -amdgpu-waitcnt-forcezero on the assembly).
+        swar: pad STATES wait states between a vector store of more than 8 bytes and a later
+        writer of its data VGPRs (the GFX9 store-data hazard, which LLVM's hazard recognizer
+        skips for MUBUF stores with an SGPR soffset).
 """
 import re
 import sys
@@ -40,6 +48,75 @@ def main():
             for r in d:
                 d[r] += n
 
+    if policy.startswith(('wz_', 'nop_')):
+        kind, cls = policy.split('_', 1)
+        ins = '\ts_waitcnt vmcnt(0) expcnt(0) lgkmcnt(0)\n' if kind == 'wz' else '\ts_nop 0\n'
+        n, meta = 0, False
+        for line in open(src):
+            out.append(line)
+            s = line.strip()
+            meta = (meta or s.startswith('.amdgpu_metadata')) and \
+                not s.startswith('.end_amdgpu_metadata')
+            if meta or not s or s[0] in ';.' or s.endswith(':') or line[0] not in ' \t':
+                continue
+            op = s.split()[0]
+            hit = {'all': not op.startswith(('s_endpgm', 's_setpc', 's_branch', 's_cbranch')),
+                   'vload': op.startswith(('buffer_load', 'global_load', 'scratch_load')),
+                   'vstore': op.startswith(('buffer_store', 'global_store', 'scratch_store',
+                                            'buffer_atomic', 'global_atomic')),
+                   'lds': op.startswith('ds_'),
+                   'smem': op.startswith(('s_load', 's_buffer_load')),
+                   'valu': op.startswith('v_') and not op.startswith('v_mfma'),
+                   'mfma': op.startswith('v_mfma')}[cls]
+            if hit:
+                out.append(ins)
+                n += 1
+        open(dst, 'w').writelines(out)
+        print('%s: %d inserted' % (policy, n))
+        return
+    if policy == 'swar':
+        pending, n = {}, 0          # data reg -> states since the store
+        for line in open(src):
+            s = line.strip()
+            if not s or s[0] in ';.' or s.endswith(':') or line[0] not in ' \t':
+                out.append(line)
+                continue
+            parts = s.split(';')[0].replace(',', ' ').split()
+            op, ops = parts[0], parts[1:]
+            dst_regs = set() if op.startswith(NO_DST) or not ops else regs(ops[0])
+            pad = max([need - pending[r] for r in dst_regs if r in pending] + [0])
+            if pad > 0:
+                out.append('\ts_nop %d\n' % (pad - 1))
+                n += 1
+                pending = {r: v + pad for r, v in pending.items()}
+            out.append(line)
+            k = int(ops[0], 0) + 1 if op == 's_nop' else 1
+            pending = {r: v + k for r, v in pending.items() if v + k < need}
+            if op.startswith(('buffer_store_dwordx3', 'buffer_store_dwordx4',
+                              'global_store_dwordx3', 'global_store_dwordx4')):
+                for r in regs(ops[0]):
+                    pending[r] = 0
+        open(dst, 'w').writelines(out)
+        print('%s: %d pads inserted' % (policy, n))
+        return
+    if policy in ('vm0', 'lgkm0', 'exp0'):
+        n = 0
+        for line in open(src):
+            st = line.strip()
+            if st.startswith('s_waitcnt ') and not line.startswith(';'):
+                new = line
+                if policy == 'vm0':
+                    new = re.sub(r'vmcnt\(\d+\)', 'vmcnt(0)', line)
+                elif policy == 'lgkm0':
+                    new = re.sub(r'lgkmcnt\(\d+\)', 'lgkmcnt(0)', line)
+                elif 'expcnt' not in line:
+                    new = line.rstrip('\n') + ' expcnt(0)\n'
+                n += new != line
+                line = new
+            out.append(line)
+        open(dst, 'w').writelines(out)
+        print('%s: %d waits rewritten' % (policy, n))
+        return
     for line in open(src):
         s = line.strip()
         is_ins = bool(s) and s[0] not in ';.' and not s.endswith(':') and line[0] in ' \t'

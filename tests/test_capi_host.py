@@ -288,6 +288,47 @@ def test_scratch_guard_catches_a_build_without_nt_loads(tmp_path):
     assert descs and bad > 0 and good == 0, (descs, good, bad)
 
 
+def test_store_data_guard_on_snippets():
+    """the build guard flags a VALU write of a 16-byte store's data VGPRs in the
+    very next instruction (MUBUF: vdata first; global: vaddr, then vdata), and nothing once a
+    wait state separates them or the writer is a load."""
+    from pntf import build
+    hz = build.store_data_hazards
+    st = "\tbuffer_store_dwordx4 v[4:7], v9, s[0:3], s5 offen nt\n"
+    assert len(hz(st + "\tv_add_f32_e32 v6, v1, v2\n")) == 1
+    assert hz(st + "\ts_nop 0\n\tv_add_f32_e32 v6, v1, v2\n") == []
+    assert hz(st + "\tv_add_f32_e32 v8, v1, v2\n") == []
+    assert hz(st + "\tbuffer_load_dwordx4 v[4:7], v9, s[0:3], 0 offen\n") == []
+    gst = "\tglobal_store_dwordx4 v[0:1], v[4:7], off\n"
+    assert hz(gst + "\tv_mov_b32_e32 v0, 0\n") == []
+    assert len(hz(gst + "\tv_accvgpr_read_b32 v5, a0\n")) == 1
+    assert hz("\tbuffer_store_dwordx2 v[4:5], v9, s[0:3], 0 offen\n\tv_mov_b32 v4, 0\n") == []
+
+
+@pytest.mark.parametrize("unit", ["wide_d3_k1", "wide_d6_k3", "fsplit_d3_k1", "gemm", "train"])
+def test_store_data_guard_clean_on_built_units(unit):
+    from pntf import build
+    assert build.store_data_hazards(_asm(unit)) == []
+
+
+def test_store_data_guard_catches_an_unguarded_build(tmp_path):
+    """Without bstore's keep-alive s_nop (-DPNTF_BSTORE_UNGUARDED) the headline wide τ+∇τ
+    kernel has the hazard that corrupted lanes 12-15: the guard must see it."""
+    import subprocess
+    from pntf import build
+    out = str(tmp_path / "variant.s")
+    cmd = ([build.hipcc()] + [f for f in build.CXXFLAGS if not f.startswith(("-save-temps",
+                                                                            "-Rpass"))]
+           + ["-DPNTF_DIM=3", "-DPNTF_KIND=1", "-DPNTF_WIDE_FIELD", "-DPNTF_PF_STEPS=2", "-DPNTF_BSTORE_UNGUARDED",
+              "--cuda-device-only", "-S", os.path.join(build.CSRC, "pntf_kernels.hip"),
+              "-o", out])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0 and "not found" in r.stderr:
+        pytest.skip("hipcc unavailable")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(build.store_data_hazards(open(out).read())) > 0
+
+
 def test_field_schedule_resolution_and_wide_index_guard():
     """AUTO's kernel choice (include/pntf.h), and the guard of ADVICE r02: the wide kernel
     keeps 32-bit tile indices, so no batch above 2^31 - 32 pairs may reach it, whatever

@@ -23,17 +23,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int H = 128;              // hidden width (model_res_sigmoid_multi.py:134)
 constexpr int TILE = 16;            // pairs per wave
 constexpr int WAVES = 4;            // waves per workgroup (one per SIMD)
-// Waves per workgroup of the split-tile kernels (pntf_split.h): one per SIMD.  8 (two per
-// SIMD) builds and is 5 % faster at 16 pairs, but returns wrong ∇τ in pair columns 12-15
-// from the second wave on a SIMD; diagnostics only.
+// Waves per workgroup of the split-tile kernels (pntf_split.h): 8, two per SIMD, so one
+// wave's LDS exchange and epilogue run beside the other's MFMAs (4: one per SIMD).  The 8-wave
+// build returned wrong ∇τ in pair columns 12-15 until the store-data hazard was found and
+// padded (pntf_field.h bstore).
 #ifndef PNTF_SPLIT
-#define PNTF_SPLIT 4
+#define PNTF_SPLIT 8
 #endif
 constexpr int SPLIT_WAVES = PNTF_SPLIT;
-// One wave per SIMD: the kernels need up to 512 VGPRs to stay spill-free.  (At two waves per
-// SIMD (256 VGPRs) hipcc spills MFMA results, and on gfx950 those spill stores read the
-// MFMA destination before its last pass lands: corrupt columns 12-15 of 16x16 tiles under
-// load — DESIGN.md §7.)
+// One wave per SIMD: the wave-tile / wide kernels need up to 512 VGPRs to stay spill-free
+// (at two waves per SIMD, 256 VGPRs, hipcc spills to scratch).
 #ifndef PNTF_WAVES_PER_SIMD
 #define PNTF_WAVES_PER_SIMD 1
 #endif

@@ -48,8 +48,8 @@ constexpr int QBUF = 2 * 16 * 68;           // activation buffer: 2 columns x 16
 constexpr int QNSIG = 48;                   // saved σ10 slots per wave (64 floats each)
 constexpr int Q_RED = 3 * QBUF + Q_WAVES * QNSIG * 64;
 constexpr int Q_BW = Q_RED + Q_WAVES * 12 * 4;   // 2π·B of the tile's 4 pairs: [pair][dim][128]
-// 24576 floats = 96 KiB: more than half the CU's LDS, so one workgroup per CU (the second
-// wave per SIMD corrupts MFMA results here)
+// 24576 floats = 96 KiB: more than half the CU's LDS, so one workgroup per CU (a second one
+// would stream the weights through the same CU a second time per step)
 constexpr int Q_LDS_FLOATS = 24576;
 static_assert(Q_BW + QPAIRS * 6 * H <= Q_LDS_FLOATS, "quad LDS budget");
 // σ slots (forward order): encoder[0] 0-3, encoder blocks a0 4-7, b0 8-11, a1 12-15,

@@ -24,9 +24,8 @@
 
 namespace pntf {
 
-// Waves sharing a pair tile: 4 (one per SIMD).  The code is written for 8 as well (two per
-// SIMD, so one wave's exchange and epilogue could run beside the other's MFMAs); that build is
-// kept for diagnostics only (pntf_common.h PNTF_SPLIT).
+// Waves sharing a pair tile: SPLIT_WAVES = 8 (two per SIMD, so one wave's exchange and
+// epilogue run beside the other's MFMAs) or 4 (one per SIMD); pntf_common.h PNTF_SPLIT.
 constexpr int SPLIT = SPLIT_WAVES;
 static_assert(SPLIT == 4 || SPLIT == 8, "split width");
 constexpr int EOTL = 8 / SPLIT;    // local out tiles of an encoder layer (OT 8, 2 columns)
@@ -60,7 +59,7 @@ __device__ float* pntf_dbg;
 typedef __attribute__((address_space(3))) float lds_f;
 typedef __attribute__((address_space(3))) f32x4 lds_f4;
 
-// Diagnostics only (DESIGN.md §7.5 bisection, tests/diag): -DPNTF_DIAG_WAITS=<bit mask> puts a
+// Diagnostics only (DESIGN.md §7.1 bisection, tests/diag): -DPNTF_DIAG_WAITS=<bit mask> puts a
 // full s_waitcnt at the marked points of the split kernels.
 #ifndef PNTF_DIAG_WAITS
 #define PNTF_DIAG_WAITS 0

@@ -13,15 +13,14 @@ Codegen guards fail the build instead of shipping a wrong kernel:
     VGPR_SPILL_ALLOWED;
   * no SGPR spills in the headline wide units (SGPR_SPILL_FREE);
   * every saved-σ scratch load carries the nt policy (scratch_policy_violations);
-  * no packed-fp32 VALU ops (v_pk_{mul,add,fma}_f32) in device code.  On gfx950 a packed op
-    that reads the result of a transcendental (v_exp/v_log/v_rcp/v_sin/v_cos) issued a few
-    instructions earlier sees stale values in lanes 12-15 of every 16-lane row; ROCm 7.2's
-    hazard recognizer under-pads that pair (measured: tests/diag).  Packed-fp32
-    codegen is therefore disabled for the device (-packed-fp32-ops), which costs nothing here;
+  * no packed-fp32 VALU ops (v_pk_{mul,add,fma}_f32) in device code: round 1 blamed them for
+    the lanes 12-15 corruption that the store-data guard below explains; the
+    device is still compiled with -packed-fp32-ops, which costs nothing here;
   * no vector store of more than 8 bytes whose data VGPRs the very next instruction overwrites
     (store_data_hazards).  On gfx950 that overwrite corrupts the stored data in lanes 12-15 of
     every 16-lane row; LLVM's hazard recognizer pads the pair except for MUBUF stores with an
-    SGPR soffset, so every buffer store passes soffset 0 (measured: tests/diag).
+    SGPR soffset, so every 16-byte buffer store is followed by an s_nop that reads its data
+    (pntf_field.h bstore; measured: tests/diag).
 A summary of every kernel's registers and spills is written to build/report.json.
 """
 import argparse
@@ -68,7 +67,7 @@ def _vregs(tok):
 
 
 def store_data_hazards(asm):
-    """Store-data guard (DESIGN.md §7.5): (line, instruction) of every VALU instruction that
+    """Store-data guard (DESIGN.md §7.1): (line, instruction) of every VALU instruction that
     writes a data VGPR of a vector store of more than 8 bytes with no wait state between them (an
     s_nop k gives k + 1).  Straight-line over the listing, so a store at the end of a block and
     the first instruction of the next are also paired (conservative)."""

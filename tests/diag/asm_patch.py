@@ -9,7 +9,7 @@ POLICY: none | allmfma (STATES after every MFMA) | raw (non-MFMA reader of an MF
         result) | war (non-MFMA writer of a register an MFMA read; warv: VMEM loads excluded) | valu2mfma (MFMA reading a
         register a non-MFMA wrote) — each pads the instruction pair to at least STATES
         (default 24) wait states.  Counting is straight-line (labels do not reset it).
-        Waitcnt rewrites (DESIGN.md §7.5 bisection): vm0 / lgkm0 turn every compiler-emitted
+        Waitcnt rewrites (DESIGN.md §7.1 bisection): vm0 / lgkm0 turn every compiler-emitted
         partial vmcnt / lgkmcnt wait into a full one, exp0 adds expcnt(0) to every s_waitcnt.
         After-class inserts: wz_<cls> puts a full s_waitcnt 0 after, nop_<cls> an s_nop 0 after,
         every instruction of class cls = all | vload | vstore | lds | smem | valu | mfma (wz_all

@@ -1,6 +1,6 @@
 """Split-tile τ+∇τ code objects (tests/diag/hsaco_<name>.hsaco from build_asm.sh, built with
 -DPERF_SPLIT [-DPNTF_SPLIT=8]) against the library's wave-tile kernel on the same pairs:
-max relative ∇τ error by pair lane.  Diagnostics only (DESIGN.md §7.5):
+max relative ∇τ error by pair lane.  Diagnostics only (DESIGN.md §7.1):
     python tests/diag/split_hsaco.py <split> <name> ..."""
 import ctypes, os, sys
 import numpy as np

@@ -289,7 +289,7 @@ def test_scratch_guard_catches_a_build_without_nt_loads(tmp_path):
 
 
 def test_store_data_guard_on_snippets():
-    """DESIGN §7.5: the build guard flags a VALU write of a 16-byte store's data VGPRs in the
+    """DESIGN §7.1: the build guard flags a VALU write of a 16-byte store's data VGPRs in the
     very next instruction (MUBUF: vdata first; global: vaddr, then vdata), and nothing once a
     wait state separates them or the writer is a load."""
     from pntf import build
@@ -313,7 +313,7 @@ def test_store_data_guard_clean_on_built_units(unit):
 
 def test_store_data_guard_catches_an_unguarded_build(tmp_path):
     """Without bstore's keep-alive s_nop (-DPNTF_BSTORE_UNGUARDED) the headline wide τ+∇τ
-    kernel has the hazard that corrupted lanes 12-15 (DESIGN §7.5): the guard must see it."""
+    kernel has the hazard that corrupted lanes 12-15 (DESIGN §7.1): the guard must see it."""
     import subprocess
     from pntf import build
     out = str(tmp_path / "variant.s")

@@ -435,6 +435,107 @@ __global__ __launch_bounds__(256, PNTF_PANEL_WPS) void panel_gemm_kernel(PanelAr
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// LDS panel GEMM: the same per-wave formulation with the weight held in LDS.  Workgroup b
+// serves one 128-column group of C (4 out tiles); it copies that group's packed fragments
+// (KC/2 KiB: 128 KiB at KC = 256) from P into LDS once, then its 4 waves stride over the
+// 32-row tiles.  Per iteration a wave reads its 4 fragments with ds_read_b128 (one iteration
+// ahead), so the only vector-memory loads in the loop are the A panels: a panel's float4 q is
+// reloaded for the next tile right after its MFMAs, a whole tile (QK iterations, ~15 µs at
+// KC = 256) before it is needed, and the in-order vmcnt never couples a weight read to an HBM
+// panel read (the register-stream kernel above waits on both).  With two groups (NC = 256)
+// the workgroups of a tile's two groups sit on the same XCD (block ids 8 apart), so the second
+// panel read of a tile hits that XCD's L2.
+template <int KC, int NC, bool ACC>
+__global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
+  constexpr int QK = KC / 8, NG = NC / 128, FR = 4 * QK;
+  static_assert(QK >= 8, "C prefetch distance");
+  __shared__ f32x4 lw[FR * 64];
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // block b -> (group, workgroup index): XCD = b % 8 (dispatch order); within an XCD's
+  // blocks, consecutive pairs are the two groups of one set of tiles
+  int grp = 0, wg = blockIdx.x, nwg = gridDim.x;
+  if constexpr (NG == 2) {
+    const int x = blockIdx.x & 7, s = blockIdx.x >> 3;
+    grp = s & 1;
+    wg = (s >> 1) * 8 + x;
+    nwg = gridDim.x / 2;
+  }
+  {   // stage the group's fragments (contiguous in P: out tiles 4·grp .. 4·grp + 3)
+    const f32x4* src = g.P + (int64_t)grp * FR * 64;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < FR * 64; i += 256) lw[i] = src[i];
+  }
+  __syncthreads();
+  const int64_t ntiles = (g.M + 31) / 32;
+  const int64_t stride = (int64_t)nwg * 4;
+  int64_t tile = (int64_t)wg * 4 + w;
+  if (tile >= ntiles) return;   // wave-uniform; no barrier follows
+  auto win = [&](const float* base, int64_t ld, int64_t t) {
+    const int64_t rows = g.M - 32 * t;
+    return pg_rsrc(base + 32 * t * ld, (rows < 32 ? rows : 32) * ld * 4);
+  };
+  const int va = (int)((j * g.lda + 4 * h) * 4), vc = (int)((j * g.ldc + 4 * h) * 4);
+  const int c0 = 128 * grp;   // first out column of the group
+  f32x4 x[QK];
+  {
+    const Rsrc ra = win(g.A, g.lda, tile);
+#pragma unroll
+    for (int q = 0; q < QK; ++q) x[q] = pg_load(ra, va, 32 * q);
+  }
+  const f32x4* lf = lw + lane;
+  f32x4 fr[2][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) fr[0][t] = lf[(t * QK) * 64];
+  for (;;) {
+    const int64_t next = tile + stride;
+    const bool more = next < ntiles;
+    const Rsrc rn = win(g.A, g.lda, more ? next : tile);
+    const Rsrc rc = win(g.C, g.ldc, tile);
+    f32x16 acc[4];
+    f32x4 cb[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    pg_static_for<0, QK>([&](auto I) {
+      constexpr int q = decltype(I)::value, cur = q & 1;
+      if constexpr (ACC && q == QK - 4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int R = 0; R < 4; ++R) cb[t][R] = pg_load(rc, vc, (c0 + 32 * t + 8 * R) * 4);
+      }
+      // next iteration's fragments (past the tile's end: the next tile's first ones)
+      constexpr int qn = (q + 1) % QK;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fr[cur ^ 1][t] = lf[(t * QK + qn) * 64];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[cur][t][e], x[q][e], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (more) x[q] = pg_load(rn, va, 32 * q);   // x[q] is dead for this tile: next panel
+      if constexpr (q == QK - 1) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int R = 0; R < 4; ++R) {
+            f32x4 v = {acc[t][4 * R], acc[t][4 * R + 1], acc[t][4 * R + 2], acc[t][4 * R + 3]};
+            if (ACC) v += cb[t][R];
+            pg_store(rc, v, vc, (c0 + 32 * t + 8 * R) * 4);
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (!more) break;
+    tile = next;
+  }
+}
+
 thread_local char g_err[512] = "";
 
 // CU count of the current device, cached per device (queried on every GEMM otherwise).
@@ -476,16 +577,18 @@ int64_t splits_for(int64_t M, int64_t N, int64_t K) {
 
 // The panel path serves the forward / input-gradient shapes: K, N ∈ {128, 256}, dense rows,
 // beta 0 or 1, 16-byte aligned operands.  PNTF_GEMM_PANEL=0 in the environment turns it off
-// (the LDS-tiled kernel then runs every shape; used to compare the two).
+// (the LDS-tiled kernel then runs every shape; used to compare), 1 selects the register-stream
+// panel kernel instead of the LDS one.
 bool panel_shape(int64_t N, int64_t K) {
   return (K == 128 || K == 256) && (N == 128 || N == 256);
 }
-bool panel_enabled() {
-  static const int on = [] {
+// PNTF_GEMM_PANEL: 0 = off, 1 = the register-stream panel kernel, 2 (default) = the LDS one.
+int panel_mode() {
+  static const int mode = [] {
     const char* e = getenv("PNTF_GEMM_PANEL");
-    return e && e[0] == '0' ? 0 : 1;
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
   }();
-  return on != 0;
+  return mode;
 }
 
 }  // namespace pntf_gemm
@@ -514,7 +617,7 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
     snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: null pointer");
     return PNTF_ERR_ARG;
   }
-  if (!ta && (beta == 0.f || beta == 1.f) && panel_shape(N, K) && panel_enabled() &&
+  if (!ta && (beta == 0.f || beta == 1.f) && panel_shape(N, K) && panel_mode() != 0 &&
       lda == K && ldc == N && work && work_floats >= (size_t)(K * N) &&
       ((uintptr_t)A & 15) == 0 && ((uintptr_t)C & 15) == 0 && ((uintptr_t)work & 15) == 0) {
     const int64_t nf = (N / 32) * (K / 8) * 64;
@@ -522,6 +625,30 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
                        stream, B, ldb, tb, (int)K, (int)N, reinterpret_cast<f32x4*>(work));
     PanelArgs p{A, reinterpret_cast<const f32x4*>(work), C, M, lda, ldc};
     const int64_t tiles = (M + 31) / 32, wgs = (tiles + 3) / 4;
+    if (panel_mode() == 2) {
+      // one workgroup per CU (128 KiB of LDS at K = 256); per group at most CUs / NG of them
+      // a multiple of 8 so that a tile's two group workgroups share an XCD (N = 256)
+      // (K = 128 without C: 64 KiB of LDS and ≤ 256 registers, so two per CU)
+      const int64_t ng = N / 128, cap = (K == 128 && beta == 0.f ? 2 : 1) * num_cus() / ng;
+      int64_t nwg = wgs < cap ? wgs : cap;
+      if (ng == 2) nwg = (nwg + 7) / 8 * 8;
+      const dim3 grid((unsigned)(nwg * ng));
+#define PNTF_PANEL(KC, NC)                                                                      \
+  if (beta != 0.f) hipLaunchKernelGGL((panel_lds_kernel<KC, NC, true>), grid, dim3(256), 0,      \
+                                      stream, p);                                               \
+  else hipLaunchKernelGGL((panel_lds_kernel<KC, NC, false>), grid, dim3(256), 0, stream, p);
+      if (K == 128 && N == 128) { PNTF_PANEL(128, 128) }
+      else if (K == 128) { PNTF_PANEL(128, 256) }
+      else if (N == 128) { PNTF_PANEL(256, 128) }
+      else { PNTF_PANEL(256, 256) }
+#undef PNTF_PANEL
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: %s", hipGetErrorString(e));
+        return PNTF_ERR_HIP;
+      }
+      return PNTF_OK;
+    }
     const int64_t slots = (int64_t)PNTF_PANEL_WPS * num_cus();
     const unsigned grid = (unsigned)(wgs < slots ? wgs : slots);
 #define PNTF_PANEL(KC, NC)                                                                     \

@@ -433,8 +433,10 @@ def test_training_uses_no_vendor_gemm():
         torch.cuda.synchronize()
     names = [e.key for e in prof.key_averages()]
     assert any("gemm_kernel" in n for n in names), names
-    # forward / input-gradient Linears run on the register-panel kernel
-    assert any("panel_gemm_kernel" in n for n in names), names
+    # forward / input-gradient Linears run on the LDS panel kernel (PNTF_GEMM_PANEL=1: the
+    # register-stream one)
+    panel = "panel_gemm_kernel" if os.environ.get("PNTF_GEMM_PANEL") == "1" else "panel_lds_kernel"
+    assert any(panel in n for n in names), names
     assert not any("Cijk" in n or "hipblaslt" in n.lower() for n in names), names
 
 

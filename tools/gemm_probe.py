@@ -6,6 +6,13 @@ import sys
 import torch
 
 
+def SHAPES(pairs):
+    """(tag, rows, K, N) of the dim-3 tape (pntf/train.py): R = 5 planes over the 2·pairs
+    encoder points, R = 9 over the pairs after the merge."""
+    return (("gen", 9 * pairs, 256, 256), ("enc", 5 * 2 * pairs, 128, 128),
+            ("enc0", 5 * 2 * pairs, 256, 128), ("g3", 9 * pairs, 256, 128))
+
+
 def timeit(fn, reps=10):
     fn()
     torch.cuda.synchronize()
@@ -22,8 +29,7 @@ def main():
     dev = torch.device("cuda:0")
     pairs = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
     out = {}
-    for tag, rows, K, N in (("gen", 13 * pairs, 256, 256), ("enc", 7 * 2 * pairs, 128, 128),
-                            ("enc0", 7 * 2 * pairs, 256, 128), ("g3", 13 * pairs, 256, 128)):
+    for tag, rows, K, N in SHAPES(pairs):
         X = torch.randn(rows, K, device=dev)
         G = torch.randn(rows, N, device=dev)
         W = torch.randn(N, K, device=dev)
@@ -52,8 +58,7 @@ def split_probe(pairs=20000):
     from pntf.train import weight_grad
     dev = torch.device("cuda:0")
     out = {}
-    for tag, rows, K, N in (("gen", 13 * pairs, 256, 256), ("enc", 7 * 2 * pairs, 128, 128),
-                            ("enc0", 7 * 2 * pairs, 256, 128), ("g3", 13 * pairs, 256, 128)):
+    for tag, rows, K, N in SHAPES(pairs):
         X = torch.randn(rows, K, device=dev)
         G = torch.randn(rows, N, device=dev)
         GW = torch.empty(N, K, device=dev)
@@ -73,8 +78,7 @@ def mfma_probe(pairs=20000):
     from pntf.train import gemm
     dev = torch.device("cuda:0")
     out = {}
-    for tag, rows, K, N in (("gen", 13 * pairs, 256, 256), ("enc", 7 * 2 * pairs, 128, 128),
-                            ("enc0", 7 * 2 * pairs, 256, 128), ("g3", 13 * pairs, 256, 128)):
+    for tag, rows, K, N in SHAPES(pairs):
         X = torch.randn(rows, K, device=dev)
         G = torch.randn(rows, N, device=dev)
         W = torch.randn(N, K, device=dev)
@@ -101,8 +105,23 @@ def mfma_probe(pairs=20000):
     print(json.dumps(out, indent=1))
 
 
+def one_probe(pairs=20000, reps=5):
+    """The generator forward shape alone on the library GEMM (for PMC passes)."""
+    sys.path.insert(0, __file__.rsplit("/tools/", 1)[0] + "/p-ntfields_amd")
+    from pntf.train import gemm
+    dev = torch.device("cuda:0")
+    _, rows, K, N = SHAPES(pairs)[0]
+    X = torch.randn(rows, K, device=dev)
+    W = torch.randn(N, K, device=dev)
+    Y = torch.empty(rows, N, device=dev)
+    fl = 2.0 * rows * K * N / 1e9
+    print(json.dumps({"gen_fwd_TFLOPs": fl / timeit(lambda: gemm(Y, X, W, False, True), reps)}))
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 2 and sys.argv[2] == "mfma":
+    if len(sys.argv) > 2 and sys.argv[2] == "one":
+        one_probe(int(sys.argv[1]))
+    elif len(sys.argv) > 2 and sys.argv[2] == "mfma":
         mfma_probe(int(sys.argv[1]))
     else:
         main()

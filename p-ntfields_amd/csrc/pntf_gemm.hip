@@ -6,8 +6,11 @@
 //   weight gradient  gW (N x K)    = gYᵀ · X  over all rows     (A = gYᵀ, B row-major, split-K)
 // C = beta·C + A·B with A(m, k) = TA ? A[k·lda + m] : A[m·lda + k] and
 // B(k, n) = TB ? B[n·ldb + k] : B[k·ldb + n].
+// Three kernels serve them: the LDS panel kernel (forward and input gradient, K, N ∈ {128,
+// 256}), the register-streamed wgrad kernel (weight gradients, M, N ∈ {128, 256}) and, for
+// every other shape / operand, the LDS-tiled kernel described next.
 //
-// Workgroup tile 128 x 128, K chunks of 8 staged through LDS (double-buffered, one barrier per
+// LDS-tiled kernel: workgroup tile 128 x 128, K chunks of 8 staged through LDS (double-buffered, one barrier per
 // chunk, the next chunk's global loads in flight during the current chunk's MFMAs); 4 waves,
 // each a 64 x 64 block = 2 x 2 MFMA tiles of 32 x 32 (64 accumulators).  Per chunk and wave:
 // 16 MFMAs of 64 cycles; the chunk's LDS operands are read before its MFMAs (one latency per
@@ -536,6 +539,167 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Weight-gradient GEMM  gW (M x N) = gYᵀ (M x rows) · X (rows x N), M, N ∈ {128, 256}: the
+// reduction runs over every Taylor row of the tape (10⁵-10⁶), the output is one or a few
+// 128 x 128 tiles.  No LDS staging and no barrier in the loop: one wave owns a whole 128 x 128
+// output tile (4 x 4 MFMA tiles = 256 accumulators) and streams its rows straight from HBM.
+// Per row pair (k step of v_mfma_f32_32x32x2_f32, lane half h = row 2p + h) a lane loads ONE
+// float4 of gY (out rows 4j .. 4j+3) and ONE float4 of X (out cols 4j .. 4j+3); component e of
+// the first is the A operand of out rows {4i + e}, component d of the second the B operand of
+// out cols {4j + d}, so the two 1 KiB wave loads feed all 16 MFMAs (1024 MFMA cycles per
+// 2 KiB: the stream needs 8 B/clk per CU, far below L2 / HBM rates).  Three register buffers
+// of one 16-row chunk each; a buffer is refilled in one burst right after its MFMAs, two
+// chunks ahead of its use.  Workgroup b = (split s, tile): its 4 waves take the
+// 16-row chunks of the split's row range round-robin (adjacent waves read adjacent rows), then
+// sum their tiles through LDS in a fixed order (w0, + w1, + w2, + w3) and write one partial
+// (M x N layout) per split; gemm_reduce1/2 sum the splits in order (deterministic).
+// D register r of lane (j, h) for tile (e, d) is out row 4·((r & 3) + 8·(r >> 2) + 4h) + e,
+// out col 4j + d: a float4 over d is one 16-byte store of consecutive columns.
+struct WgradArgs {
+  const float* A;   // gY (rows x M), row stride M
+  const float* B;   // X (rows x N), row stride N
+  float* work;      // splits x (M x N) partial sums
+  int64_t rows, rps;  // reduction length; rows per split (a multiple of 128)
+  int M, N;
+  int xcd;            // splits a multiple of 8: XCD-aware block -> (split, tile) map
+};
+constexpr int WG_PF = 8;   // row pairs per chunk = ring slots
+
+__device__ __forceinline__ void wg_store(float* p, f32x4 v) {
+  *reinterpret_cast<f32x4*>(p) = v;
+  asm volatile("s_nop 0" ::"v"(v));   // store-data hazard guard (pntf_field.h bstore)
+}
+
+template <int T, int NB>
+__global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs g) {
+  __shared__ f32x4 red[2][64 * 64];   // two 128 x 128 tiles (128 KiB)
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // block b runs on XCD b % 8 (dispatch order): with the split count a multiple of 8 the T
+  // tiles of one split take blocks 8 apart, so they share an XCD and its L2 serves the second
+  // read of each gY / X row segment
+  const int b8 = blockIdx.x >> 3;
+  const int tile = g.xcd ? b8 % T : blockIdx.x % T;
+  const int s = g.xcd ? (blockIdx.x & 7) + 8 * (b8 / T) : blockIdx.x / T;
+  const int tnn = g.N / 128, tm = tile / tnn, tn = tile % tnn;
+  const int64_t r0 = (int64_t)s * g.rps;
+  const int64_t left = g.rows - r0;
+  const int64_t nrows = left <= 0 ? 0 : (left < g.rps ? left : g.rps);
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[e][d][r] = 0.f;
+  if (nrows > 0) {
+    // rows past the split's end are outside the resources: their loads return 0
+    const Rsrc ra = pg_rsrc(g.A + r0 * g.M, nrows * g.M * 4);
+    const Rsrc rb = pg_rsrc(g.B + r0 * g.N, nrows * g.N * 4);
+    const int va = (h * g.M + 128 * tm + 4 * j) * 4, vb = (h * g.N + 128 * tn + 4 * j) * 4;
+    const int sa = __builtin_amdgcn_readfirstlane(2 * g.M * 4);
+    const int sb = __builtin_amdgcn_readfirstlane(2 * g.N * 4);
+    const int nchunks = (int)((nrows + 2 * WG_PF - 1) / (2 * WG_PF));
+    int c = w;
+    if constexpr (NB == 1) {
+      // ring of WG_PF slots: slot p is refilled with the wave's next chunk right after its
+      // MFMAs, WG_PF - 1 row pairs ahead of its use.  Loads past the range fall outside the
+      // resources (zeros, no memory access), so they stay unconditional and vmcnt exact.
+      f32x4 xa[WG_PF], xb[WG_PF];
+      if (c < nchunks) {
+#pragma unroll
+        for (int p = 0; p < WG_PF; ++p) {
+          xa[p] = pg_load(ra, va, (c * WG_PF + p) * sa);
+          xb[p] = pg_load(rb, vb, (c * WG_PF + p) * sb);
+        }
+      }
+      for (; c < nchunks; c += 4) {
+        const int na = (c + 4) * WG_PF * sa, nb = (c + 4) * WG_PF * sb;
+        pg_static_for<0, WG_PF>([&](auto I) {
+          constexpr int p = decltype(I)::value;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+              acc[e][d] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[p][e], xb[p][d], acc[e][d], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          xa[p] = pg_load(ra, va, na + p * sa);
+          xb[p] = pg_load(rb, vb, nb + p * sb);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      }
+    } else {
+      // two chunk buffers, each refilled in one burst (16 rows of both operands) right after
+      // its MFMAs, one chunk ahead of its use
+      f32x4 xa[2][WG_PF], xb[2][WG_PF];
+      // buffer indices are compile-time (a runtime index would put the arrays in scratch)
+      auto fill = [&](auto B, int ch) {
+        constexpr int buf = decltype(B)::value;
+#pragma unroll
+        for (int p = 0; p < WG_PF; ++p) {
+          xa[buf][p] = pg_load(ra, va, (ch * WG_PF + p) * sa);
+          xb[buf][p] = pg_load(rb, vb, (ch * WG_PF + p) * sb);
+        }
+      };
+      auto run = [&](auto B) {
+        constexpr int buf = decltype(B)::value;
+        pg_static_for<0, WG_PF>([&](auto I) {
+          constexpr int p = decltype(I)::value;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+              acc[e][d] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[buf][p][e], xb[buf][p][d],
+                                                               acc[e][d], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      };
+      constexpr std::integral_constant<int, 0> b0{};
+      constexpr std::integral_constant<int, 1> b1{};
+      if (c < nchunks) {
+        fill(b0, c);
+        fill(b1, c + 4);
+      }
+      for (; c < nchunks; c += 8) {
+        run(b0);
+        fill(b0, c + 8);
+        run(b1);   // unconditional (a branch here doubles the accumulators); the rows per
+                   // split are a multiple of 128, so only the last split runs a zero chunk
+        fill(b1, c + 12);
+      }
+    }
+  }
+  // fixed-order sum of the four waves' tiles, (w0 + w2) + (w1 + w3), through LDS without
+  // writing the accumulators back (a read-modify-write of 256 of them spilled): w2, w3 store
+  // their tiles; w0, w1 add theirs into those in place; then wave w adds the two halves for
+  // out rows 4i + w and writes them to the split's partial
+  auto at = [&](int e, int r) { return (e * 16 + r) * 64 + lane; };
+  auto quad = [&](int e, int r) {
+    return f32x4{acc[e][0][r], acc[e][1][r], acc[e][2][r], acc[e][3][r]};
+  };
+  if (w >= 2) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[w - 2][at(e, r)] = quad(e, r);
+  }
+  __syncthreads();
+  if (w < 2) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[w][at(e, r)] += quad(e, r);
+  }
+  __syncthreads();
+  float* out = g.work + (int64_t)s * g.M * g.N + 128 * tn + 4 * j;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = 128 * tm + 4 * ((r & 3) + 8 * (r >> 2) + 4 * h) + w;
+    wg_store(out + (int64_t)m * g.N, red[0][at(w, r)] + red[1][at(w, r)]);
+  }
+}
+
 thread_local char g_err[512] = "";
 
 // CU count of the current device, cached per device (queried on every GEMM otherwise).
@@ -591,6 +755,38 @@ int panel_mode() {
   return mode;
 }
 
+// The weight-gradient kernel serves gYᵀ·X with M, N ∈ {128, 256} (ta, not tb, beta 0, dense
+// 16-byte aligned operands).  PNTF_GEMM_WGRAD=0 in the environment sends those shapes to the
+// LDS-tiled split-K kernel instead (used to compare the two).
+bool wgrad_shape(int64_t M, int64_t N) {
+  return (M == 128 || M == 256) && (N == 128 || N == 256);
+}
+bool wgrad_enabled() {
+  static const int on = [] {
+    const char* e = getenv("PNTF_GEMM_WGRAD");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+// Refill scheme per tile count: the two-buffer burst for the 256 x 256 gradients (T = 4:
+// 206 vs 215 µs at 9 x 20 000 rows), the per-slot ring for T = 1, 2 (64 vs 67, 103 vs 106 µs;
+// tools/wgrad_prof.sh).  PNTF_WGRAD_RING=1 or 2 forces one of them (to compare).
+int wgrad_ring(int T) {
+  static const int force = [] {
+    const char* e = getenv("PNTF_WGRAD_RING");
+    return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
+  }();
+  return force ? force : (T == 4 ? 2 : 1);
+}
+// one workgroup per CU over all tiles, at least 256 rows per split
+int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t T = (M / 128) * (N / 128);
+  int64_t s = num_cus() / T;
+  const int64_t kmax = (K + 255) / 256;
+  if (s > kmax) s = kmax;
+  return s < 1 ? 1 : s;
+}
+
 }  // namespace pntf_gemm
 
 using namespace pntf_gemm;
@@ -602,7 +798,9 @@ size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K) {
   const int64_t s = splits_for(M, N, K);
   const size_t split = s > 1 ? (size_t)(s * M * N) : 0;
   const size_t packed = panel_shape(N, K) ? (size_t)(K * N) : 0;
-  return split > packed ? split : packed;
+  const size_t wgrad = wgrad_shape(M, N) ? (size_t)((wgrad_splits(M, N, K) + 7) * M * N) : 0;
+  const size_t big = split > packed ? split : packed;
+  return big > wgrad ? big : wgrad;
 }
 
 int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
@@ -666,6 +864,42 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
       return PNTF_ERR_HIP;
     }
     return PNTF_OK;
+  }
+  if (ta && !tb && beta == 0.f && wgrad_shape(M, N) && wgrad_enabled() && lda == M &&
+      ldb == N && work && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 &&
+      ((uintptr_t)work & 15) == 0) {
+    // rows per split: a multiple of 128 (4 waves x two 16-row chunks); the buffer offsets are
+    // 32-bit, so a split must stay below 2 GiB of either operand
+    const int64_t s0 = wgrad_splits(M, N, K);
+    int64_t rps = ((K + s0 - 1) / s0 + 127) / 128 * 128;
+    int64_t s = (K + rps - 1) / rps;
+    // XCD-aware map: pad the split count to a multiple of 8 (empty splits write zeros)
+    const bool xcd = (M / 128) * (N / 128) > 1 && s >= 8;
+    if (xcd) s = (s + 7) / 8 * 8;
+    if (rps * (M > N ? M : N) * 4 < ((int64_t)1 << 31) - ((int64_t)1 << 20) &&
+        work_floats >= (size_t)(s * M * N)) {
+      const int T = (int)((M / 128) * (N / 128));
+      WgradArgs wa{A, B, work, K, rps, (int)M, (int)N, (int)xcd};
+      const dim3 grid((unsigned)(s * T));
+#define PNTF_WGRAD(NB)                                                                          \
+  if (T == 1) hipLaunchKernelGGL((wgrad_kernel<1, NB>), grid, dim3(256), 0, stream, wa);         \
+  else if (T == 2) hipLaunchKernelGGL((wgrad_kernel<2, NB>), grid, dim3(256), 0, stream, wa);    \
+  else hipLaunchKernelGGL((wgrad_kernel<4, NB>), grid, dim3(256), 0, stream, wa);
+      if (wgrad_ring(T) == 2) { PNTF_WGRAD(2) } else { PNTF_WGRAD(1) }
+#undef PNTF_WGRAD
+      const int64_t n = M * N;
+      const unsigned nb = (unsigned)((n + 255) / 256);
+      hipLaunchKernelGGL(gemm_reduce1_kernel, dim3(nb, (unsigned)((s + RG - 1) / RG)),
+                         dim3(256), 0, stream, work, (int)s, n);
+      hipLaunchKernelGGL(gemm_reduce2_kernel, dim3(nb), dim3(256), 0, stream, work, (int)s, M,
+                         N, C, ldc, beta);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: %s", hipGetErrorString(e));
+        return PNTF_ERR_HIP;
+      }
+      return PNTF_OK;
+    }
   }
   // the LDS-tiled kernel puts the row tiles on grid.y (HIP limit 65535): M above
   // 65535 * 128 ≈ 8.4M rows cannot launch there (the panel path above has no such limit)

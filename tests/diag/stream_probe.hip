@@ -60,10 +60,12 @@ int main() {
   (void)hipMalloc(&w, FLOATS * 4);
   (void)hipMemset(w, 0, FLOATS * 4);
   (void)hipMalloc(&out, 1024 * 256 * 4);
-  for (int g : {1, 64, 256}) {
+  for (int g : {1, 64, 256, 512}) {
     run<4>(w, out, g);
     run<8>(w, out, g);
     run<16>(w, out, g);
+    run<32>(w, out, g);
+    run<48>(w, out, g);
   }
   return 0;
 }

@@ -393,6 +393,9 @@ def test_arm_model_train_two_epochs(tmp_path):
     (False, False, 1, 256, 128, 0.0),
     (True, False, 256, 256, 260013, 0.0),   # weight gradient gYᵀ·X (split-K)
     (True, False, 128, 256, 1000, 0.0),     # weight gradient, short reduction
+    (True, False, 128, 128, 200003, 0.0),   # weight gradient kernel, one 128 x 128 tile
+    (True, False, 256, 128, 65, 0.0),       # ... two tiles, one ragged split
+    (True, False, 128, 128, 3, 0.0),        # ... fewer rows than one 16-row chunk
     (True, True, 128, 128, 77, 0.5),
 ])
 def test_mfma_gemm_vs_fp64(ta, tb, M, N, K, beta):
@@ -416,9 +419,26 @@ def test_mfma_gemm_vs_fp64(ta, tb, M, N, K, beta):
 
 
 @pytest.mark.gpu
+def test_weight_grad_deterministic():
+    """The weight-gradient GEMM sums its per-wave tiles and its splits in a fixed order (LDS
+    adds between barriers, gemm_reduce1/2): two launches on the same operands are bitwise
+    equal (the reference's CPU autograd is deterministic too)."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(5)
+    G = torch.randn(90001, 256, generator=g).to(dev)
+    X = torch.randn(90001, 256, generator=g).to(dev)
+    a = torch.empty(256, 256, device=dev)
+    b = torch.empty(256, 256, device=dev)
+    train.weight_grad(G, X, a)
+    train.weight_grad(G, X, b)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
 def test_training_uses_no_vendor_gemm():
     """The training step's GEMMs are the library's own MFMA kernels: a profiled
-    Loss + backward launches gemm_kernel (weight gradients) and panel_gemm_kernel (forward,
+    Loss + backward launches wgrad_kernel (weight gradients) and panel_lds_kernel (forward,
     input gradients) and no Tensile (Cijk_*) / hipBLASLt kernel."""
     from torch.profiler import ProfilerActivity, profile
     dev = torch.device("cuda:0")
@@ -432,7 +452,10 @@ def test_training_uses_no_vendor_gemm():
         loss.backward()
         torch.cuda.synchronize()
     names = [e.key for e in prof.key_averages()]
-    assert any("gemm_kernel" in n for n in names), names
+    # weight gradients on the register-streamed wgrad kernel (PNTF_GEMM_WGRAD=0: the LDS-tiled
+    # split-K gemm_kernel)
+    wg = "gemm_kernel" if os.environ.get("PNTF_GEMM_WGRAD") == "0" else "wgrad_kernel"
+    assert any(wg in n for n in names), names
     # forward / input-gradient Linears run on the LDS panel kernel (PNTF_GEMM_PANEL=1: the
     # register-stream one)
     panel = "panel_gemm_kernel" if os.environ.get("PNTF_GEMM_PANEL") == "1" else "panel_lds_kernel"

@@ -32,6 +32,15 @@ if __name__ == "__main__":
                             mode=ops.GRAD_EXACT, schedule=sched)
     ms = bench._timeit(c5, reps=reps)
     st = res["p"][1]
+    # active queries per step and the step at which at most one query per CU is left (the
+    # tail hand-off point of the AUTO schedule)
+    import numpy as np
+    sc = st.cpu().numpy()
+    active = [int((sc > s).sum()) for s in range(int(sc.max()) + 1)]
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    handoff = next((s for s, a in enumerate(active) if a <= cus), None)
+    print(json.dumps({"active_per_step": active[::5], "handoff_step": handoff,
+                      "steps_hist": np.bincount(sc // 10).tolist()}), flush=True)
     print(json.dumps({"c5_ms": ms, "schedule": sched, "mean_steps": float(st.float().mean()),
                       "max_steps": int(st.max()), "query_steps": int(st.sum()),
                       "us_per_step": 1e3 * ms / int(st.max())}), flush=True)

@@ -249,6 +249,20 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
                  size_t work_floats, hipStream_t stream);
 const char* pntf_tt_gemm_last_error(void);
 
+/* One Linear of the Taylor tape with its bias, residual and act_laplace fused (the forward
+ * GEMM of pntf_tt_gemm followed by pntf_tt_act_fwd, in one kernel; :663-691, :744/:828):
+ * x (R, m, k) planes, W (n, k) the torch weight (y = x·Wᵀ), bias (n), res (R, m, n) or NULL
+ * -> y (R, m, n) pre-activation (value plane + bias, every plane + res; kept as the tape) and,
+ * when act != 0, h (R, m, n) the softplus10 Taylor rows.  R = 1 + ndir + nl with (ndir, nl) =
+ * (3|6, 1) or (6|12, 2); k, n in {128, 256}; all pointers 16-byte aligned; `work` holds the
+ * packed weight (k*n floats).  act == 0 requires res == NULL (h unused).  schedule: 0 = AUTO
+ * (the fused kernel when its 32-point blocks balance over the waves, else the two kernels),
+ * 1 = always the fused kernel, 2 = always pntf_tt_gemm + pntf_tt_act_fwd; errors of either
+ * path are reported by pntf_tt_gemm_last_error / pntf_tt_last_error respectively. */
+int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const float* W,
+                       int n, const float* bias, const float* res, float* y, float* h, int act,
+                       int schedule, float* work, size_t work_floats, hipStream_t stream);
+
 /* torch.optim.AdamW update of one parameter tensor (the reference's optimizer, :959-961):
  * p, grad, exp_avg, exp_avg_sq (n); `step` = the step count after this update (>= 1). */
 int pntf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,

@@ -540,6 +540,169 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Linear + act_laplace of the Taylor tape in one pass (pntf_tt_linear_act; the forward of one
+// Linear of NN.out_laplace, model_res_sigmoid_multi.py:710-848 with act_laplace :675-691).
+// The LDS panel GEMM above with the tape's elementwise stage as its epilogue, so the
+// pre-activation never round-trips HBM between the GEMM and a separate act kernel.  A wave
+// owns a 32-POINT block and runs the block's R planes one after the other, in the order
+//   value, then per endpoint group l: its GK = ndir/nl first-derivative (J) planes, its
+//   summed second-derivative (L) plane,
+// so everything the act of a plane needs is already in the wave: lane (j, h) holds point j's
+// 64 features of the group (D register 4R + e of out tile t = column 32t + 8R + 4h + e), and
+// keeps per feature σ(10 y₀) from the value plane and Σ_{k∈l} J_k² over the group's J planes:
+//   value  y₀ = acc + bias (+ res)   h = softplus₁₀(y₀)          s = σ(10 y₀)
+//   J_k    y  = acc (+ res)          h = s·y                      jj += y²
+//   L_l    y  = acc (+ res)          h = 10 s(1 - s)·jj + s·y
+// y (the tape) and h are both stored; the residual planes are loaded 4 iterations before the
+// store, like the ACC path's C.  Same formulas as tt_act_fwd_kernel (pntf_train.hip).
+struct ActArgs {
+  const float* A;      // x planes (R·M, KC)
+  const f32x4* P;      // packed weight fragments (panel_pack_kernel)
+  float* Y;            // pre-activation planes (R·M, NC)
+  float* H;            // activation planes (R·M, NC), act only
+  const float* bias;   // (NC)
+  const float* res;    // residual planes (R·M, NC) or null
+  int64_t M;           // points per plane
+  int R, ndir, nl, act;
+};
+
+__device__ __forceinline__ float pa_sig10(float y) { return 1.f / (1.f + expf(-10.f * y)); }
+__device__ __forceinline__ float pa_softplus10(float y) {
+  return 10.f * y > 20.f ? y : log1pf(expf(10.f * y)) / 10.f;
+}
+
+template <int KC, int NC>
+__global__ __launch_bounds__(256, 1) void panel_act_kernel(ActArgs g) {
+  constexpr int QK = KC / 8, NG = NC / 128, FR = 4 * QK;
+  static_assert(QK >= 8, "residual prefetch distance");
+  __shared__ f32x4 lw[FR * 64];
+  __shared__ f32x4 lb[32];   // the group's 128 biases
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int grp = 0, wg = blockIdx.x, nwg = gridDim.x;
+  if constexpr (NG == 2) {   // a block's two groups on one XCD (panel_lds_kernel)
+    const int x = blockIdx.x & 7, s = blockIdx.x >> 3;
+    grp = s & 1;
+    wg = (s >> 1) * 8 + x;
+    nwg = gridDim.x / 2;
+  }
+  {
+    const f32x4* src = g.P + (int64_t)grp * FR * 64;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < FR * 64; i += 256) lw[i] = src[i];
+    if (threadIdx.x < 32)
+      lb[threadIdx.x] = reinterpret_cast<const f32x4*>(g.bias)[grp * 32 + threadIdx.x];
+  }
+  __syncthreads();
+  const int64_t nblk = (g.M + 31) / 32;
+  const int64_t stride = (int64_t)nwg * 4;
+  int64_t blk = (int64_t)wg * 4 + w;
+  if (blk >= nblk) return;   // wave-uniform; no barrier follows
+  const int R = g.R, ndir = g.ndir, GK = g.ndir / g.nl;
+  const bool has_res = g.res != nullptr, act = g.act != 0;
+  // plane at sequence position i: 0, then per group l its GK J planes and its L plane
+  auto plane_of = [&](int i) {
+    if (i == 0) return 0;
+    const int l = (i - 1) / (GK + 1), k = (i - 1) % (GK + 1);
+    return k < GK ? 1 + l * GK + k : 1 + ndir + l;
+  };
+  // the 32-row window of (block b, plane r); rows past the plane's M are outside it
+  auto win = [&](const float* base, int ld, int64_t b, int r) {
+    const int64_t rows = g.M - 32 * b;
+    return pg_rsrc(base + ((int64_t)r * g.M + 32 * b) * ld, (rows < 32 ? rows : 32) * ld * 4);
+  };
+  const int va = (j * KC + 4 * h) * 4, vc = (j * NC + 4 * h) * 4;
+  const int c0 = 128 * grp;
+  f32x4 x[QK];
+  {
+    const Rsrc ra = win(g.A, KC, blk, 0);
+#pragma unroll
+    for (int q = 0; q < QK; ++q) x[q] = pg_load(ra, va, 32 * q);
+  }
+  const f32x4* lf = lw + lane;
+  f32x4 fr[2][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) fr[0][t] = lf[(t * QK) * 64];
+  f32x4 s[4][4], jj[4][4];   // per feature of point j: σ(10 y₀), Σ J² of the current group
+  int i = 0;
+  for (;;) {
+    const int r = plane_of(i);
+    int ni = i + 1;
+    int64_t nb = blk;
+    if (ni == R) {
+      ni = 0;
+      nb = blk + stride;
+    }
+    const bool more = nb < nblk;
+    const Rsrc rn = win(g.A, KC, more ? nb : blk, more ? plane_of(ni) : r);
+    const Rsrc ry = win(g.Y, NC, blk, r), rh = win(g.H, NC, blk, r);
+    const Rsrc rr = win(has_res ? g.res : g.Y, NC, blk, r);
+    // plane kind: 0 value, 1 J (first of its group: 2), 3 L
+    const int kind = r == 0 ? 0 : r <= ndir ? ((r - 1) % GK == 0 ? 2 : 1) : 3;
+    f32x16 acc[4];
+    f32x4 cb[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+    pg_static_for<0, QK>([&](auto I) {
+      constexpr int q = decltype(I)::value, cur = q & 1;
+      if constexpr (q == QK - 4) {
+        if (has_res) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int Q = 0; Q < 4; ++Q) cb[t][Q] = pg_load(rr, vc, (c0 + 32 * t + 8 * Q) * 4);
+        }
+      }
+      constexpr int qn = (q + 1) % QK;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fr[cur ^ 1][t] = lf[(t * QK + qn) * 64];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[cur][t][e], x[q][e], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (more) x[q] = pg_load(rn, va, 32 * q);
+      if constexpr (q == QK - 1) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int Q = 0; Q < 4; ++Q) {
+            f32x4 v = {acc[t][4 * Q], acc[t][4 * Q + 1], acc[t][4 * Q + 2], acc[t][4 * Q + 3]};
+            if (kind == 0) v += lb[8 * t + 2 * Q + h];   // (acc + bias) + res, as tt_act_fwd
+            if (has_res) v += cb[t][Q];
+            const int off = (c0 + 32 * t + 8 * Q) * 4;
+            pg_store(ry, v, vc, off);
+            if (act) {
+              f32x4 hv;
+              if (kind == 0) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  s[t][Q][e] = pa_sig10(v[e]);
+                  hv[e] = pa_softplus10(v[e]);
+                }
+              } else if (kind == 3) {
+                hv = 10.f * s[t][Q] * (1.f - s[t][Q]) * jj[t][Q] + v * s[t][Q];
+              } else {
+                hv = v * s[t][Q];
+                jj[t][Q] = kind == 2 ? v * v : jj[t][Q] + v * v;
+              }
+              pg_store(rh, hv, vc, off);
+            }
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (!more) break;
+    i = ni;
+    blk = nb;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Weight-gradient GEMM  gW (M x N) = gYᵀ (M x rows) · X (rows x N), M, N ∈ {128, 256}: the
 // reduction runs over every Taylor row of the tape (10⁵-10⁶), the output is one or a few
 // 128 x 128 tiles.  No LDS staging and no barrier in the loop: one wave owns a whole 128 x 128
@@ -942,6 +1105,60 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: %s", hipGetErrorString(e));
+    return PNTF_ERR_HIP;
+  }
+  return PNTF_OK;
+}
+
+int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const float* W,
+                       int n, const float* bias, const float* res, float* y, float* h, int act,
+                       int schedule, float* work, size_t work_floats, hipStream_t stream) {
+  const bool planes = (nl == 1 && (ndir == 3 || ndir == 6)) ||
+                      (nl == 2 && (ndir == 6 || ndir == 12));
+  const auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!planes || m < 0 || !panel_shape(n, k) || (m > 0 && (!x || !W || !bias || !y || !work ||
+      (act && !h))) || (res && !act) || work_floats < (size_t)k * n ||
+      !al(x) || !al(bias) || !al(res) || !al(y) || !al(h) || !al(work)) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: bad arguments");
+    return PNTF_ERR_ARG;
+  }
+  if (schedule < 0 || schedule > 2) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: unknown schedule");
+    return PNTF_ERR_ARG;
+  }
+  if (m == 0) return PNTF_OK;
+  const int R = 1 + ndir + nl;
+  // A wave of the fused kernel owns whole 32-point blocks (all R planes), so it balances only
+  // when every wave gets about the same number of blocks: at the reference batch (625 blocks
+  // of the generator's 20 000 points on 512 waves per column group) a fifth of the waves
+  // would run two blocks and the rest one.  AUTO takes the fused kernel when the blocks fill
+  // their rounds to >= 90 %, otherwise the GEMM (32-row tiles of every plane, balanced) and
+  // the act kernel.
+  const int64_t blocks = (m + 31) / 32, wgs = (blocks + 3) / 4;
+  const int64_t ng = n / 128, cap = num_cus() / ng;
+  int64_t nwg = wgs < cap ? wgs : cap;
+  if (ng == 2) nwg = (nwg + 7) / 8 * 8;
+  const int64_t waves = 4 * nwg, rounds = (blocks + waves - 1) / waves;
+  const bool fused = schedule == 1 || (schedule == 0 && 10 * blocks >= 9 * rounds * waves);
+  if (!fused) {
+    int st = pntf_tt_gemm(0, 1, R * m, n, k, x, k, W, k, y, n, 0.f, work, work_floats, stream);
+    if (st) return st;
+    return pntf_tt_act_fwd(ndir, nl, y, h, bias, res, m, n, act, stream);
+  }
+  const int64_t nf = (int64_t)(n / 32) * (k / 8) * 64;
+  hipLaunchKernelGGL(panel_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0,
+                     stream, W, (int64_t)k, 1, k, n, reinterpret_cast<f32x4*>(work));
+  ActArgs a{x, reinterpret_cast<const f32x4*>(work), y, h, bias, res, m, R, ndir, nl, act};
+  // as the LDS panel GEMM: one workgroup per CU per column group (a multiple of 8 workgroups
+  // per group for two groups); each wave strides over 32-point blocks
+  const dim3 grid((unsigned)(nwg * ng));
+  if (k == 128 && n == 128) hipLaunchKernelGGL((panel_act_kernel<128, 128>), grid, dim3(256), 0, stream, a);
+  else if (k == 128) hipLaunchKernelGGL((panel_act_kernel<128, 256>), grid, dim3(256), 0, stream, a);
+  else if (n == 128) hipLaunchKernelGGL((panel_act_kernel<256, 128>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((panel_act_kernel<256, 256>), grid, dim3(256), 0, stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: %s", hipGetErrorString(e));
     return PNTF_ERR_HIP;
   }
   return PNTF_OK;

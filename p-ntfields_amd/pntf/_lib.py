@@ -80,6 +80,10 @@ SIGNATURES = {
                                     _c_void_p, _i64, _c_void_p, _i64, _f32, _c_void_p,
                                     ctypes.c_size_t, _c_void_p]),
     "pntf_tt_gemm_last_error": (ctypes.c_char_p, []),
+    "pntf_tt_linear_act": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _i64, ctypes.c_int,
+                                          _c_void_p, ctypes.c_int, _c_void_p, _c_void_p, _c_void_p,
+                                          _c_void_p, ctypes.c_int, ctypes.c_int, _c_void_p,
+                                          ctypes.c_size_t, _c_void_p]),
     "pntf_adamw": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32,
                                   _f32, _f32, _f32, _i64, _c_void_p]),
     # speed-sample generator (pntf_mesh.hip)

@@ -27,6 +27,7 @@ The GEMMs are the library's own fp32 MFMA kernels (pntf_tt_gemm: v_mfma_f32_32x3
 is a HIP kernel of libpntf.so (csrc/pntf_train.hip).  There is no CPU path and no vendor GEMM.
 """
 import ctypes
+import os
 
 import torch
 
@@ -34,6 +35,10 @@ from . import _lib, ops
 from ._lib import PntfError, check
 
 H = 128
+# Schedule of the forward Linear + act (pntf_tt_linear_act): 0 AUTO (the fused kernel where its
+# 32-point blocks balance over the waves), 1 always fused, 2 always pntf_tt_gemm +
+# pntf_tt_act_fwd (the y planes round-trip HBM).  PNTF_TT_FUSED sets it (to compare).
+_LINEAR_ACT = int(os.environ.get("PNTF_TT_FUSED", "0"))
 _BLOCK_HEADS = ("encoder.1", "encoder.2", "generator.0", "generator.1", "generator.2")
 
 
@@ -111,9 +116,16 @@ class _Tape:
         ndir, nl = self.planes(R)
         y = torch.empty((R, M, N), dtype=torch.float32, device=self.dev)
         h = torch.empty_like(y) if act else None
-        gemm(y.view(R * M, N), x3.view(R * M, K), W, ta=False, tb=True)
-        check(self.lib.pntf_tt_act_fwd(ndir, nl, _vp(y), _vp(h), _vp(b), _vp(res), M, N,
-                                       int(act), self.s), "pntf_tt_act_fwd")
+        # GEMM + bias + residual + act_laplace (pntf_tt_linear_act: one fused kernel, or the
+        # GEMM and the act kernel where the fused one would not balance)
+        work = _work(self.dev, int(self.lib.pntf_tt_gemm_work_floats(R * M, N, K)))
+        st = self.lib.pntf_tt_linear_act(ndir, nl, _vp(x3), M, K, _vp(W), N, _vp(b), _vp(res),
+                                         _vp(y), _vp(h), int(act), _LINEAR_ACT, _vp(work),
+                                         work.numel(), self.s)
+        if st != 0:
+            raise PntfError("pntf_tt_linear_act: %s | %s" % (
+                self.lib.pntf_tt_gemm_last_error().decode(),
+                self.lib.pntf_tt_last_error().decode()))
         self.ops.append((name, x3, y, act, res is not None))
         return h if act else y
 

@@ -419,6 +419,34 @@ def test_mfma_gemm_vs_fp64(ta, tb, M, N, K, beta):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,dim", CASES)
+def test_fused_linear_act_matches_two_kernel_path(name, dim, monkeypatch):
+    """pntf_tt_linear_act (GEMM + bias + residual + act_laplace in one kernel) against the
+    two-kernel path it replaces (pntf_tt_gemm + pntf_tt_act_fwd): same loss terms and weight
+    gradients to fp32 rounding, for the encoder (dim planes) and generator (2·dim planes)
+    layouts of both models, at init and trained (W2) weights."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    f = load(name)
+    model, net = _nets(dim, _case_weights(name), dev, f["B"] if dim == 6 else None)
+    out = {}
+    for fused in (True, False):
+        monkeypatch.setattr(train, "_LINEAR_ACT", 1 if fused else 2)
+        for p in net.parameters():
+            p.grad = None
+        loss, _, diff = _loss(model, f, dim, dev)
+        loss.backward()
+        out[fused] = (diff.detach().clone(),
+                      [p.grad.detach().clone() for p in net.parameters() if p.grad is not None])
+    d1, g1 = out[True]
+    d0, g0 = out[False]
+    assert torch.allclose(d1, d0, rtol=1e-5, atol=1e-6)
+    assert len(g1) == len(g0)
+    for a, b in zip(g1, g0):
+        assert float((a - b).norm() / b.norm().clamp_min(1e-30)) < 1e-5
+
+
+@pytest.mark.gpu
 def test_weight_grad_deterministic():
     """The weight-gradient GEMM sums its per-wave tiles and its splits in a fixed order (LDS
     adds between barriers, gemm_reduce1/2): two launches on the same operands are bitwise

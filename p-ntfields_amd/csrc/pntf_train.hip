@@ -235,37 +235,41 @@ __global__ __launch_bounds__(256) void tt_act_bwd_kernel(const float* __restrict
 }
 
 // out[j] (+)= Σ_b partial[b][j], deterministic: workgroup x owns columns 64x..64x+63 (one per
-// lane, coalesced rows); wave w sums the rows b ≡ w (mod 4) in order, 4 loads in flight; the
-// four wave sums are combined in fixed order through LDS.
-__global__ __launch_bounds__(256) void reduce_kernel(const float* __restrict__ partial, int nb,
-                                                     int W, float* __restrict__ out,
-                                                     int accumulate) {
+// lane, coalesced rows); wave w of RW sums the rows b ≡ w (mod RW) in order, 4 loads in
+// flight; the wave sums are combined in fixed order through LDS.  RW = 16 waves: a 512-row
+// partial is 8 rounds of 4 loads per wave (the 4-wave version ran 11 µs, latency-bound).
+constexpr int RW = 16;
+__global__ __launch_bounds__(64 * RW) void reduce_kernel(const float* __restrict__ partial,
+                                                         int nb, int W, float* __restrict__ out,
+                                                         int accumulate) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (j < W) {
     int b = w;
-    for (; b + 12 < nb; b += 16) {
+    for (; b + 3 * RW < nb; b += 4 * RW) {
       s0 += partial[(int64_t)b * W + j];
-      s1 += partial[(int64_t)(b + 4) * W + j];
-      s2 += partial[(int64_t)(b + 8) * W + j];
-      s3 += partial[(int64_t)(b + 12) * W + j];
+      s1 += partial[(int64_t)(b + RW) * W + j];
+      s2 += partial[(int64_t)(b + 2 * RW) * W + j];
+      s3 += partial[(int64_t)(b + 3 * RW) * W + j];
     }
-    for (; b < nb; b += 4) s0 += partial[(int64_t)b * W + j];
+    for (; b < nb; b += RW) s0 += partial[(int64_t)b * W + j];
   }
-  __shared__ float red[4][64];
+  __shared__ float red[RW][64];
   red[w][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (w == 0 && j < W) {
-    const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < RW; k += 2) s += red[k][lane] + red[k + 1][lane];
     out[j] = accumulate ? out[j] + s : s;
   }
 }
 
 void launch_reduce(const float* partial, int nb, int W, float* out, int accumulate,
                    hipStream_t stream) {
-  hipLaunchKernelGGL(reduce_kernel, dim3((W + 63) / 64), dim3(256), 0, stream, partial, nb, W,
-                     out, accumulate);
+  hipLaunchKernelGGL(reduce_kernel, dim3((W + 63) / 64), dim3(64 * RW), 0, stream, partial, nb,
+                     W, out, accumulate);
 }
 
 // ---------------------------------------------------------------- start/goal merge (:761-811)

@@ -229,18 +229,27 @@ class EikonalLossFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xp, yobs, Btab, env, dim, gamma, scale, arm, keys, *params):
         p = {k: t.detach() for k, t in zip(keys, params)}
-        grads = {k: torch.empty_like(t) for k, t in p.items()}
+        # all weight gradients in one flat buffer (views at 256-byte aligned offsets), so that
+        # backward scales them by the incoming gradient in one launch instead of one per tensor
+        offs, n = [], 0
+        for k in keys:
+            offs.append(n)
+            n += (p[k].numel() + 63) // 64 * 64
+        flat = torch.empty(n, dtype=torch.float32, device=xp.device)
+        grads = {k: flat[o:o + p[k].numel()].view(p[k].shape) for k, o in zip(keys, offs)}
         diff = loss_grad(p, xp, yobs, Btab, env, dim, gamma, scale, arm, grads)
-        ctx.grads = [grads[k] for k in keys]
+        ctx.flat, ctx.offs = flat, offs
+        ctx.shapes = [p[k].shape for k in keys]
         ctx.mark_non_differentiable(diff)
         total = ops.device_sum(diff).float() * scale
         return total, diff
 
     @staticmethod
     def backward(ctx, g_total, g_diff):
-        gs = ctx.grads
-        ctx.grads = None
-        return (None,) * 9 + tuple(g * g_total for g in gs)
+        flat = ctx.flat * g_total
+        ctx.flat = None
+        gs = [flat[o:o + sh.numel()].view(sh) for o, sh in zip(ctx.offs, ctx.shapes)]
+        return (None,) * 9 + tuple(gs)
 
 
 def eikonal_loss(module, xp, yobs, Btab, env, dim, gamma, scale, arm=False):

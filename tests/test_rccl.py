@@ -71,3 +71,51 @@ def test_rccl_world1_allgather():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+def _gpu_worker(rank, world, port, n, q):
+    """One rank of the sharded path on the box's single GPU: its contiguous shard through the
+    HIP kernels (the same entry points bench.py's ranks call), then the all-gather of the
+    per-rank rows (gloo over host copies: two RCCL ranks cannot share one device)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as tdist
+    from pntf import dist, ops, synth
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    assert dist.init("gloo") == (rank, world)
+    W = synth.make_weights(0)
+    packed = ops.pack_weights([torch.from_numpy(v).to(dev) for v in W.values()])
+    xp = torch.from_numpy(synth.make_pairs(n, 3, seed=5)).to(dev)
+    Bt = torch.from_numpy(synth.make_B_table(10, 3)).to(dev)
+    e = torch.from_numpy(synth.make_env_ids(n, 10)).to(dev)
+    lo, hi = dist.shard_range(n, rank, world)
+    # one schedule for the shards and the whole batch: per-pair results are then bitwise equal
+    t, d = ops.tau_grad(packed, xp[lo:hi], Bt, e[lo:hi], dim=3, schedule="wide_tile")
+    full = dist.all_gather_rows(torch.cat([t.unsqueeze(1), d], 1).cpu(), n)
+    tf, df = ops.tau_grad(packed, xp, Bt, e, dim=3, schedule="wide_tile")
+    assert torch.equal(full, torch.cat([tf.unsqueeze(1), df], 1).cpu())
+    # planner queries sharded the same way (uneven shards)
+    Ba = torch.from_numpy(synth.make_B(6, seed=12, arm=True).T.copy()).to(dev)
+    xq = torch.from_numpy(synth.make_box_pairs(q, 6, seed=3)).to(dev)
+    lo, hi = dist.shard_range(q, rank, world)
+    kw = dict(dim=6, step=0.015, tol=0.03, max_iter=40, mode=ops.GRAD_EXACT,
+              schedule="quad_tile")
+    path, steps = ops.plan(packed, xq[lo:hi], Ba, **kw)
+    gp = dist.all_gather_rows(path.cpu(), q)
+    gs = dist.all_gather_rows(steps.cpu(), q)
+    pf, sf = ops.plan(packed, xq, Ba, **kw)
+    assert torch.equal(gs, sf.cpu()) and torch.equal(gp, pf.cpu())
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_share_gpu_sharded_path():
+    """bench.py's N > 1 data path (contiguous shards, per-rank HIP kernels, all-gather of the
+    per-rank rows) with two rank processes on the one GPU: the gathered τ+∇τ rows and planner
+    paths equal the single-process results bitwise."""
+    import torch.multiprocessing as mp
+    from test_dist import _free_port
+    mp.start_processes(_gpu_worker, args=(2, _free_port(), 5001, 37), nprocs=2, join=True,
+                       start_method="spawn")

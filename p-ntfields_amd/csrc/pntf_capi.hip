@@ -92,7 +92,7 @@ static int64_t wide_grid_for(int64_t n) {
   return wgs < cap ? (wgs < 1 ? 1 : wgs) : cap;
 }
 
-// quad grid (pntf_quad.h): 4-pair tiles, one 4-wave workgroup per tile, at most one per CU
+// quad grid (pntf_quad.h): 4-pair tiles, one Q_WAVES-wave workgroup per tile, at most one per CU
 static int64_t quad_grid_for(int64_t n) {
   int64_t ntiles = (n + 3) / 4;
   int64_t cap = (int64_t)num_cus();
@@ -176,7 +176,7 @@ static int check_common(const float* packed, int dim, const float* xp, int64_t n
 
 template <int DIM>
 static void launch_quad(int kind, int64_t grid, const FieldArgs& a, hipStream_t s) {
-  dim3 g((unsigned)grid), b(256);
+  dim3 g((unsigned)grid), b(64 * Q_WAVES);
   switch (kind) {
     case K_TAU: hipLaunchKernelGGL((field_quad_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
     case K_TAU_GRAD: hipLaunchKernelGGL((field_quad_kernel<DIM, K_TAU_GRAD>), g, b, 0, s, a); break;
@@ -431,7 +431,7 @@ int pntf_plan_ex(const float* packed, int dim, const float* xp0, int64_t q, cons
              (float*)ws, nullptr, 0};
   if (use_quad(q, schedule)) {
     const int64_t cus = num_cus();
-    dim3 g((unsigned)quad_grid_for(q)), b(256);
+    dim3 g((unsigned)quad_grid_for(q)), b(64 * Q_WAVES);
     if (schedule == PNTF_SCHED_AUTO && q <= cus && solo_enabled()) {
       // one query per CU (the reference's Q = 1 loop, small batches): VALU SOLO layers
       dim3 gs((unsigned)q);

@@ -74,11 +74,18 @@ constexpr int W_SZ_G4W = 16 * 256;
 constexpr int W_OFF_G4B = W_OFF_G4W + W_SZ_G4W;
 constexpr int W_SZ = W_OFF_G4B + 4;
 // Quad blob (pntf_quad.h, v_mfma_f32_4x4x1_16b_f32 on 4-pair tiles), packed after the wide
-// one: per wave of a workgroup, the fragments of its quarter of every layer's out rows in
-// the order a planner step consumes them (13 forward layers, then the 13 reverse ones), so
-// the weight ring is one linear stream; then per wave 14 bias vectors (the 13 forward
-// layers' biases and the head row, in the wave's compact row order).
-constexpr int Q_WAVES = 4;
+// one: per wave of a workgroup, the fragments of its share (1/Q_WAVES) of every layer's out
+// rows in the order a planner step consumes them (13 forward layers, then the 13 reverse
+// ones), so the weight ring is one linear stream; then per wave 14 bias vectors (the 13
+// forward layers' biases and the head row, in the wave's compact row order).
+// Q_WAVES = 8 (two per SIMD): one CU streams L2/MALL at ~130 GB/s with 8 waves loading
+// against ~103 GB/s with 4 (tests/diag/stream_probe2.hip), and a planner step is bound by
+// that stream (quad tiles).
+#ifndef PNTF_QWAVES
+#define PNTF_QWAVES 8
+#endif
+constexpr int Q_WAVES = PNTF_QWAVES;
+static_assert(Q_WAVES == 4 || Q_WAVES == 8, "quad layers: 4 or 8 waves per workgroup");
 constexpr int Q_NL = 26;
 constexpr int Q_STREAM = 2 * SZ_DIR / Q_WAVES;      // floats of one wave's fragment stream
 constexpr int Q_NF_FWD = SZ_DIR / Q_WAVES / 256;    // 1 KiB fragments of its forward part

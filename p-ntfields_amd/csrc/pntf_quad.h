@@ -11,15 +11,19 @@
 //     A lane l = W[r0 + 4·og + (l & 3)][k0 + kb], B lane l = act[k0 + kb][pair l & 3], so
 //     one instruction is 16 out rows x 4 k x 4 pairs and the accumulators hold one partial
 //     sum per k sub-block (kb), summed over the row (two DPP row_ror adds) after the layer;
-//   * the four waves of the workgroup (one per SIMD) own a quarter of every layer's out
-//     rows; after the sum each lane keeps one (row, pair) value ("compact": row
+//   * the Q_WAVES = 8 waves of the workgroup (two per SIMD) own an eighth of every layer's
+//     out rows; after the sum each lane keeps one (row, pair) value ("compact": row
 //     r0 + 4·og + kb, pair l & 3), runs the epilogue on it and writes it to an LDS
 //     activation buffer laid out for the next layer's B reads (one ds_read_b128 per 4 k and
-//     column, conflict-free), then one workgroup barrier per layer;
+//     column, conflict-free), then one workgroup barrier per layer.  Eight waves, not four:
+//     a planner step is bound by the CU's weight stream, and one CU reads L2/MALL at
+//     ~130 GB/s with eight waves loading against ~103 GB/s with four
+//     (tests/diag/stream_probe2.hip: 33 vs 42 µs per 4.33 MB step);
 //   * the saved σ10 values stay in LDS (compact, per wave), so there is no global scratch;
 //   * each wave's weight fragments are packed in consumption order (pntf_common.h Q_LAYERS),
-//     so the prefetch ring is one linear stream of 1 KiB fragments, 32 in flight, that wraps
-//     from the last reverse layer into the next step's encoder[0].
+//     so the prefetch ring is one linear stream of 1 KiB fragments, 16 in flight per wave
+//     (128 KiB per CU), that wraps from the last reverse layer into the next step's
+//     encoder[0].
 // 1024 queries are 256 tiles: every CU of the chip has one.  Reductions whose result every
 // lane consumes (τ, ∇τ) use xor butterflies and a fixed wave order, so all lanes of a pair
 // hold bitwise identical values and the planner's freeze/exit decisions agree in all waves.
@@ -36,22 +40,28 @@ constexpr int QCH = PNTF_Q_CHAINS;
 #ifndef PNTF_QKEEPB
 #define PNTF_QKEEPB 1
 #endif
-// Fragments in flight per wave: the ∇τ kernels (1056 fragments per step, a multiple of 32)
-// run PNTF_QRING of them; the τ-only kernels wrap every 528 fragments and run 16.
+// Fragments in flight per wave: the ∇τ kernels (4224 / Q_WAVES fragments per step) run
+// PNTF_QRING of them; the τ-only kernels wrap after the forward half and run half as many.
+// (128 KiB in flight per CU at either wave count)
 #ifndef PNTF_QRING
-#define PNTF_QRING 32
+#define PNTF_QRING (128 / PNTF_QWAVES)
 #endif
 constexpr int QRING = PNTF_QRING;
-constexpr int QRING_TAU = 16;
+constexpr int QRING_TAU = 64 / Q_WAVES;
+// stream position (mod the ring) of a layer that follows a 128 x 128 one: the first ring slot
+// of every other encoder layer
+constexpr int QH = 64 / Q_WAVES;
+// groups of 16 out rows per wave of a layer with OUT rows
+constexpr int qg(int out) { return out / (16 * Q_WAVES); }
 constexpr int Q_NF_ALL = 2 * Q_NF_FWD;
 constexpr int QBUF = 2 * 16 * 68;           // activation buffer: 2 columns x 16 lane rows x 68
 constexpr int QNSIG = 48;                   // saved σ10 slots per wave (64 floats each)
 constexpr int Q_RED = 3 * QBUF + Q_WAVES * QNSIG * 64;
 constexpr int Q_BW = Q_RED + Q_WAVES * 12 * 4;   // 2π·B of the tile's 4 pairs: [pair][dim][128]
-// 24576 floats = 96 KiB: more than half the CU's LDS, so one workgroup per CU (a second one
-// would stream the weights through the same CU a second time per step)
-constexpr int Q_LDS_FLOATS = 24576;
-static_assert(Q_BW + QPAIRS * 6 * H <= Q_LDS_FLOATS, "quad LDS budget");
+// 96 KiB (4 waves) / 135 KiB (8 waves): more than half the CU's LDS, so one workgroup per CU
+// (a second one would stream the weights through the same CU a second time per step)
+constexpr int Q_LDS_FLOATS = (Q_BW + QPAIRS * 6 * H + 64 + 1023) / 1024 * 1024;
+static_assert(Q_LDS_FLOATS >= 24576 && Q_LDS_FLOATS <= 40960, "quad LDS budget");
 // σ slots (forward order): encoder[0] 0-3, encoder blocks a0 4-7, b0 8-11, a1 12-15,
 // b1 16-19 (group·2 + column), merge switch 20-21, generator a_i 22 + 8i + g, b_i 26 + 8i + g,
 // generator[-2] 46-47.
@@ -104,10 +114,10 @@ struct QCx {
   // 2π·B[d][f] of pair j of the tile (staged once per tile by quad_stage_b)
   __device__ lds_f* bw(int j, int d) const { return lds + Q_BW + (j * 6 + d) * H; }
   // compact (row, pair) slot of a layer with OUT rows, group g, column c in a buffer read by
-  // the next layer (its in features = OUT: row stride OUT/4 + 4)
-  template <int OUT>
+  // the next layer (its in features = BUF, default OUT: row stride BUF/4 + 4)
+  template <int OUT, int BUF = OUT>
   __device__ lds_f* at(lds_f* b, int c, int g) const {
-    return b + (c * 16 + l16) * (OUT / 4 + 4) + w * (OUT / 16) + 4 * g + og;
+    return b + (c * 16 + l16) * (BUF / 4 + 4) + w * (OUT / (4 * Q_WAVES)) + 4 * g + og;
   }
 };
 
@@ -141,7 +151,8 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
   constexpr int SP = IN / 4 + 4, NQ = IN / 16;
   // B operands kept in registers for all groups of the layer when they fit (64 VGPRs):
   // one LDS read per fragment instead of one per fragment and group
-  constexpr bool KEEP = PNTF_QKEEPB && G > 1 && NC * NQ <= 16;
+  // (not in the SOLO layers at 8 waves: beside the VALU accumulators they spilled)
+  constexpr bool KEEP = PNTF_QKEEPB && G > 1 && NC * NQ <= 16 && !(SOLO && Q_WAVES == 8);
   // SOLO: every lane reads the one active pair's B operands (row kb, pair cx.sp)
   const lds_f* src = in + (SOLO ? ((cx.l16 & ~3) | cx.sp) : cx.l16) * SP;
   f32x4 xb[KEEP ? NC : 1][KEEP ? NQ : 1];
@@ -278,8 +289,8 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
 #pragma unroll
     for (int d = 0; d < DIM; ++d) xc[d] = c ? io.x[1][d] : io.x[0][d];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int f = fb + 32 * m;
+    for (int m = 0; m < 128 / (8 * Q_WAVES); ++m) {
+      const int f = fb + 8 * Q_WAVES * m;
       float q = 0.f;
 #pragma unroll
       for (int d = 0; d < DIM; ++d) q = fmaf(xc[d], cx.bw(j, d)[f], q);
@@ -292,7 +303,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[0] (:227); compat: the out_backgrad quirk (:435-438) stores σ10(softplus(y))
-  qlayer<2, 256, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
+  qlayer<2, 256, NF, qg(128), 0 % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       SpSig q = sp_sig(v[c] + pick(aux[0], g));
@@ -305,7 +316,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int la = 1 + 2 * blk, sa = QS_EBLK + 8 * blk;
-    qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         SpSig q = sp_sig(v[c] + pick(aux[la], g));
@@ -314,7 +325,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
       }
     });
     qsync();
-    qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), QH % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -326,12 +337,12 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
     qsync();
   }
   // ---- encoder[-1] (:234) and the smooth max / min merge (:236-244): u = [M | m] -> B
-  qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, qg(128), 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const float zs = v[0] + pick(aux[5], g), zg = v[1] + pick(aux[5], g);
     const float d = zs - zg;
     const float e = exp_neg10abs(d);
     const float cc = 0.1f * log1p_small(e);
-    lds_f* o = cx.at<256>(B, 0, g) - cx.w * 8;   // row r of a 128-row layer in a 256-row buffer
+    lds_f* o = cx.at<128, 256>(B, 0, g);   // row r of a 128-row layer in a 256-row buffer
     o[0] = fmaxf(zs, zg) + cc;
     o[32] = fminf(zs, zg) - cc;
     if (GRAD) {
@@ -345,13 +356,13 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   for (int i = 0; i < 3; ++i) {
     const f32x4 ba = i == 0 ? aux[6] : i == 1 ? aux[8] : aux[10];
     const f32x4 bb = i == 0 ? aux[7] : i == 1 ? aux[9] : aux[11];
-    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       SpSig q = sp_sig(v[0] + pick(ba, g));
       *cx.at<256>(A, 0, g) = q.sp;
       if (GRAD) *cx.sig(QS_GBLK + 8 * i + g) = q.sg;
     });
     qsync();
-    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       SpSig q = sp_sig(v[0] + pick(bb, g) + *o);
       *o = q.sp;
@@ -361,7 +372,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   // ---- generator[-2] + act (:251-252) and the head generator[-1] (:254-255)
   float part[1] = {0.f};
-  qlayer<1, 256, NF, 2, 16 % QR, QR, SOLO, NF == Q_NF_FWD>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+  qlayer<1, 256, NF, qg(128), QH % QR, QR, SOLO, NF == Q_NF_FWD>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
     SpSig q = sp_sig(v[0] + pick(aux[12], g));
     part[0] = fmaf(pick(aux[13], g), q.sp, part[0]);
     if (GRAD) *cx.sig(QS_G3 + g) = q.sg;
@@ -382,22 +393,22 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   // ---- head and generator[-2] (:592-613): dv = d · G4 ⊙ σ10(y3) -> A (128 rows)
   const float dd = 0.1f * tau * (1.f - tau);
 #pragma unroll
-  for (int g = 0; g < 2; ++g) *cx.at<128>(A, 0, g) = dd * pick(aux[13], g) * *cx.sig(QS_G3 + g);
+  for (int g = 0; g < qg(128); ++g) *cx.at<128>(A, 0, g) = dd * pick(aux[13], g) * *cx.sig(QS_G3 + g);
   qsync();
   // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> B
-  qlayer<1, 128, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+  qlayer<1, 128, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
     *cx.at<256>(B, 0, g) = v[0] * *cx.sig(QS_GBLK + 16 + 4 + g);
   });
   qsync();
   // ---- generator blocks, reverse (:615-618): lb: B -> A, la: A (+ B residual) -> B
 #pragma unroll 1
   for (int i = 2; i >= 0; --i) {
-    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * i + g);
     });
     qsync();
     const int sb = QS_GBLK + 8 * (i - 1) + 4;   // σ10(y2) of block i - 1 (none for i = 0)
-    qlayer<1, 256, NF, 4, 16 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       const float y = v[0] + *o;
       *o = i > 0 ? y * *cx.sig(sb + g) : y;
@@ -406,8 +417,8 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   }
   // ---- merge Jacobian (:620-627) on the wave's 128-row share: dz -> F (2 columns)
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const lds_f* u = cx.at<256>(B, 0, g) - cx.w * 8;   // row r of the 128-row map
+  for (int g = 0; g < qg(128); ++g) {
+    const lds_f* u = cx.at<128, 256>(B, 0, g);   // row r of the 128-row map
     const float dM = u[0], dm = u[32];
     const float s0 = *cx.sig(QS_S0 + g), s1 = 1.f - s0;
     *cx.at<128>(F, 0, g) = s0 * dM + s1 * dm;
@@ -415,7 +426,7 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1): F -> A
-  qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, qg(128), QH % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) *cx.at<128>(A, c, g) = v[c] * *cx.sig(QS_EBLK + 12 + 2 * g + c);
   });
@@ -425,12 +436,12 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
 #pragma unroll
   for (int blk = 1; blk >= 0; --blk) {
     const int sa = QS_EBLK + 8 * blk, sbelow = blk ? QS_EBLK + 4 : QS_E0;
-    qlayer<2, 128, NF, 2, 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) *cx.at<128>(B, c, g) = v[c] * *cx.sig(sa + 2 * g + c);
     });
     qsync();
-    qlayer<2, 128, NF, 2, 16 % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), QH % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -439,13 +450,14 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
     });
     qsync();
   }
-  // ---- encoder[0]^T fused with the Fourier Jacobian (:639-645): the wave's 64 feature rows
-  // f (sin rows f < 128 in waves 0-1, cos rows in waves 2-3), both columns
+  // ---- encoder[0]^T fused with the Fourier Jacobian (:639-645): the wave's 256/Q_WAVES
+  // feature rows f (sin rows f < 128 in the first half of the waves, cos rows in the second),
+  // both columns
   float acc[2 * DIM];
 #pragma unroll
   for (int i = 0; i < 2 * DIM; ++i) acc[i] = 0.f;
-  qlayer<2, 128, NF, 4, 0 % QR, QR, SOLO, true>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
-    const int f = cx.w * 64 + 16 * g + 4 * cx.og + cx.kb;
+  qlayer<2, 128, NF, qg(256), 0 % QR, QR, SOLO, true>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+    const int f = cx.w * (256 / Q_WAVES) + 16 * g + 4 * cx.og + cx.kb;
     const int fb = f & 127;
     float bw[DIM];
 #pragma unroll
@@ -481,7 +493,8 @@ __device__ __forceinline__ void quad_stage_b(const QCx& cx, const PairIO& io) {
 #pragma unroll
   for (int d = 0; d < DIM; ++d)
 #pragma unroll
-    for (int i = 0; i < H / 64; ++i) cx.bw(j, d)[f0 + 64 * i] = TWO_PI * io.Bw[d * H + f0 + 64 * i];
+    for (int i = 0; i < H / (16 * Q_WAVES); ++i)
+      cx.bw(j, d)[f0 + 16 * Q_WAVES * i] = TWO_PI * io.Bw[d * H + f0 + 16 * Q_WAVES * i];
 }
 
 __device__ __forceinline__ QCx quad_cx(lds_f* lds) {
@@ -499,7 +512,7 @@ __device__ __forceinline__ QCx quad_cx(lds_f* lds) {
 // τ / ∇τ / epilogues on quad tiles: one workgroup per 4-pair tile (grid-stride), same
 // outputs as field_kernel<DIM, KIND>.
 template <int DIM, int KIND>
-__global__ __launch_bounds__(256, 1) void field_quad_kernel(FieldArgs a) {
+__global__ __launch_bounds__(64 * Q_WAVES, 1) void field_quad_kernel(FieldArgs a) {
   constexpr bool GRAD = KIND != K_TAU && KIND != K_TRAVEL;
   constexpr int NF = GRAD ? Q_NF_ALL : Q_NF_FWD;
   constexpr int QR = GRAD ? QRING : QRING_TAU;
@@ -553,7 +566,7 @@ constexpr int Q_YIELD_EVERY = PNTF_Q_YIELD_EVERY;     // steps between hand-off 
 static_assert(Q_YIELD_FLAG < Q_LDS_FLOATS, "quad LDS budget");
 
 template <int DIM, bool SOLO>
-__global__ __launch_bounds__(256, 1) void plan_quad_kernel(PlanArgs a) {
+__global__ __launch_bounds__(64 * Q_WAVES, 1) void plan_quad_kernel(PlanArgs a) {
   __shared__ float smem[Q_LDS_FLOATS];
   const QCx cx = quad_cx((lds_f*)smem);
   int32_t* const tail = a.tail;
@@ -717,7 +730,7 @@ __global__ void pack_quad_aux_kernel(const float* __restrict__ plain, float* __r
                                 Q_LAYERS[12].bias, B_G4W};
   const int out = outs[L], off = offs[L];
   float v = 0.f;
-  if (g < out / 64)
+  if (g < qg(out))
     v = plain[off + w * (out / Q_WAVES) + 16 * g + 4 * (l >> 4) + ((l >> 2) & 3)];
   quad[Q_OFF_AUX + o] = v;
 }

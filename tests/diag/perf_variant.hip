@@ -29,7 +29,8 @@ extern "C" int perf_tau_grad(int grid, const float* P, const float* xp, int64_t 
 #ifdef PERF_WIDE
   hipLaunchKernelGGL((wide_field_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(256), 0, stream, a);
 #elif defined(PERF_QUAD)    // one workgroup per 4-pair tile
-  hipLaunchKernelGGL((field_quad_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL((field_quad_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(64 * Q_WAVES), 0,
+                     stream, a);
 #elif defined(PERF_SPLIT)   // one workgroup per 16-pair tile; ws: SPLIT slots per workgroup
   hipLaunchKernelGGL((field_split_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(64 * SPLIT), 0,
                      stream, a);

@@ -50,10 +50,10 @@ def test_pure_queries_without_gpu(lib):
     mats = 128 * 256 + 4 * 128 * 128 + 128 * 128 + 6 * 256 * 256 + 128 * 256
     plain = 128 + 4 * 128 + 128 + 6 * 256 + 128 + 128 + 4
     wide = 2 * mats + 19 * 256 + 16 * 256 + 4
-    # then (64-float aligned) the quad streams: both directions once more, and per wave 14
-    # bias / head fragments
+    # then (64-float aligned) the quad streams: both directions once more, and per wave (8 per
+    # quad workgroup) 14 bias / head fragments
     off_quad = (2 * mats + plain + wide + 63) // 64 * 64
-    assert lib.pntf_packed_floats() == off_quad + 2 * mats + 4 * 14 * 256
+    assert lib.pntf_packed_floats() == off_quad + 2 * mats + 8 * 14 * 256
     lib.pntf_status_string.restype = ctypes.c_char_p
     assert lib.pntf_status_string(1) == b"invalid argument"
 

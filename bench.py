@@ -45,9 +45,11 @@ BYTES_PER_PAIR = 52                # 24 B in + 4 B tau + 24 B dtau (algorithmic 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: Peak FP32 (matrix)
 METRIC = "(start,goal) tau+grad-tau evals/sec at batch=1M, Gibson 3D"
 UNIT = "pairs/s"
-# per-CU weight-stream ceiling of the planner (4.33 MB per step per CU, 16 x 1 KiB loads in
-# flight per wave; tests/diag/stream_probe.hip on MI355X)
-C5_STREAM_GBPS_PER_CU = 103.0
+# per-CU weight-stream ceiling of the planner: 4.33 MB per step per CU read by the quad
+# workgroup's 8 waves, 8-16 x 1 KiB loads in flight per wave (tests/diag/stream_probe2.hip on
+# MI355X: 131 GB/s with one workgroup, 132-134 with one on every CU; 103 with 4 waves;
+# DESIGN.md §3)
+C5_STREAM_GBPS_PER_CU = 131.0
 HEADLINE_UNIT = "wide_d3_k1"       # build unit of wide_field_kernel<3, K_TAU_GRAD> (pntf/build.py)
 
 
@@ -436,19 +438,20 @@ def extras(packed, dev):
     out["c5_arm_plan_1024q_wave_tile_ms"] = timeit(lambda: run_plan("wave_tile"), reps=2)
     out["c5_arm_plan_1024q_split_tile_ms"] = timeit(lambda: run_plan("split_tile"), reps=2)
     # the quad planner's C5 step time and its roofline: a step streams both weight directions
-    # (4.33 MB) through each tile's CU; the measured per-CU stream floor is ~42 us
-    # (tests/diag/stream_probe.hip), the 4x4x1 MFMA work ~23 us
+    # (4.33 MB) through each tile's CU; the measured per-CU stream floor is ~33 us with the
+    # tile's 8 waves loading (tests/diag/stream_probe2.hip), the 4x4x1 MFMA work ~17 us at the
+    # fp32 MFMA peak
     out["c5_arm_plan_us_per_step"] = 1e3 * ms / max(int(steps.max()), 1)
     # the roofline that binds this kernel is the per-CU weight stream, not the MFMA: every
-    # step of the critical path streams the CU's 4 x 1056 fragments of 1 KiB (both weight
-    # directions, pntf_quad.h) from L2/MALL; its ceiling is the measured per-CU stream rate
-    # (tests/diag/stream_probe.hip), not a datasheet number
+    # step of the critical path streams the CU's 4224 fragments of 1 KiB (both weight
+    # directions, 8 waves x 528, pntf_quad.h) from L2/MALL; its ceiling is the measured per-CU
+    # stream rate (tests/diag/stream_probe2.hip), not a datasheet number
     step_bytes = 4 * 1056 * 1024
     achieved = step_bytes / (out["c5_arm_plan_us_per_step"] * 1e-6) / 1e9
     out["c5_arm_plan_roofline"] = {
         "bound": "per-CU L2/MALL weight stream", "unit": "GB/s per CU",
         "bytes_per_step": step_bytes, "achieved": achieved, "peak": C5_STREAM_GBPS_PER_CU,
-        "peak_source": "measured stream floor (tests/diag/stream_probe.hip)",
+        "peak_source": "measured 8-wave stream floor (tests/diag/stream_probe2.hip)",
         "frac": achieved / C5_STREAM_GBPS_PER_CU}
     # batch-1 Gibson planner (test/gib_plan.py runs Q = 1): device time per loop step
     x1 = torch.from_numpy(synth.make_pairs(1, 3, seed=21)).to(dev)

@@ -267,6 +267,12 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
  * p, grad, exp_avg, exp_avg_sq (n); `step` = the step count after this update (>= 1). */
 int pntf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                float beta2, float eps, float weight_decay, int64_t step, hipStream_t stream);
+/* The same update for `count` (<= 64) tensors sharing lr, betas, eps, weight decay and step
+ * (torch.optim.AdamW's per-parameter loop over one param group, :959-961) in one launch:
+ * p[k], g[k], m[k], v[k] hold n[k] floats each (host arrays of device pointers). */
+int pntf_adamw_multi(int count, float* const* p, const float* const* g, float* const* m,
+                     float* const* v, const int64_t* n, float lr, float beta1, float beta2,
+                     float eps, float weight_decay, int64_t step, hipStream_t stream);
 
 /* ---- Speed-sample generator (pntf_mesh.hip) ---------------------- */
 

@@ -86,6 +86,9 @@ SIGNATURES = {
                                           ctypes.c_size_t, _c_void_p]),
     "pntf_adamw": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32,
                                   _f32, _f32, _f32, _i64, _c_void_p]),
+    "pntf_adamw_multi": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                        _c_void_p, _f32, _f32, _f32, _f32, _f32, _i64,
+                                        _c_void_p]),
     # speed-sample generator (pntf_mesh.hip)
     "pntf_point_mesh_distance": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _c_void_p,
                                                 ctypes.c_int, _c_void_p]),

@@ -273,7 +273,8 @@ def eikonal_loss(module, xp, yobs, Btab, env, dim, gamma, scale, arm=False):
 
 class AdamW(torch.optim.Optimizer):
     """torch.optim.AdamW semantics (the reference's optimizer, :959-961) with the update as one
-    fused HIP kernel per parameter (pntf_adamw).  Parameters without a gradient are skipped,
+    fused HIP launch per param group (pntf_adamw_multi: every tensor of the group whose step
+    counts agree; pntf_adamw per tensor otherwise).  Parameters without a gradient are skipped,
     exactly as torch does (encoder1.0).  state_dict()/load_state_dict() work as in torch, so
     the reference's rollback of (network, optimizer) states (:1093-1101) is unchanged."""
 
@@ -289,21 +290,44 @@ class AdamW(torch.optim.Optimizer):
         lib = _lib.load()
         for group in self.param_groups:
             b1, b2 = group["betas"]
+            hyper = (float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                     float(group["weight_decay"]))
+            todo = []
             for p in group["params"]:
                 if p.grad is None:
                     continue
                 ops._require_device(p, "param")
+                if not p.is_contiguous():
+                    raise PntfError("AdamW: parameters must be contiguous")
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["step"] += 1
-                g = p.grad.contiguous()
-                check(lib.pntf_adamw(_vp(p), _vp(g), _vp(st["exp_avg"]), _vp(st["exp_avg_sq"]),
-                                     p.numel(), float(group["lr"]), float(b1), float(b2),
-                                     float(group["eps"]), float(group["weight_decay"]),
-                                     int(st["step"].item()), _stream(p.device)), "pntf_adamw")
+                todo.append((p, p.grad.contiguous(), st, int(st["step"].item())))
+            if not todo:
+                continue
+            steps = {t[3] for t in todo}
+            same_dev = len({t[0].device for t in todo}) == 1
+            if len(steps) == 1 and same_dev:
+                # one launch per 64 tensors (the model's 28 trained tensors: one)
+                for c0 in range(0, len(todo), 64):
+                    chunk = todo[c0:c0 + 64]
+                    k = len(chunk)
+                    arr = lambda xs: (ctypes.c_void_p * k)(*xs)  # noqa: E731
+                    check(lib.pntf_adamw_multi(
+                        k, arr([_vp(t[0]) for t in chunk]), arr([_vp(t[1]) for t in chunk]),
+                        arr([_vp(t[2]["exp_avg"]) for t in chunk]),
+                        arr([_vp(t[2]["exp_avg_sq"]) for t in chunk]),
+                        (ctypes.c_int64 * k)(*[t[0].numel() for t in chunk]), *hyper,
+                        chunk[0][3], _stream(chunk[0][0].device)), "pntf_adamw_multi")
+            else:
+                for p, g, st, step in todo:
+                    check(lib.pntf_adamw(_vp(p), _vp(g), _vp(st["exp_avg"]),
+                                         _vp(st["exp_avg_sq"]), p.numel(), *hyper, step,
+                                         _stream(p.device)), "pntf_adamw")
+            for t in todo:
                 # the kernel wrote through a raw pointer: tell torch (and PackedCache)
-                torch.autograd.graph.increment_version(p)
+                torch.autograd.graph.increment_version(t[0])
         return loss

@@ -212,6 +212,37 @@ def test_adamw_kernel_vs_torch():
 
 
 @pytest.mark.gpu
+def test_adamw_multi_tensor_and_ragged_steps_vs_torch():
+    """The one-launch group update (pntf_adamw_multi, equal step counts) and the per-tensor
+    fallback (step counts differ: a tensor without a gradient in the first step) both agree
+    with torch.optim.AdamW; a group of 70 tensors takes two launches."""
+    from pntf import _lib
+    from pntf.train import AdamW
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(9)
+    shapes = [(256, 256), (7,), (1,)] + [(3, 5)] * 67
+    p0 = [torch.randn(s, generator=g) for s in shapes]
+    ours = [torch.nn.Parameter(p.clone().to(dev)) for p in p0]
+    ref = [torch.nn.Parameter(p.clone().to(dev)) for p in p0]
+    o1 = AdamW(ours, lr=2e-3, weight_decay=0.05)
+    o2 = torch.optim.AdamW(ref, lr=2e-3, weight_decay=0.05, foreach=False)
+    for it in range(4):
+        gs = [torch.randn(s, generator=g) * 1e-2 for s in shapes]
+        for j, (a, b, gg) in enumerate(zip(ours, ref, gs)):
+            skip = it == 0 and j == 1          # tensor 1 starts one step late
+            a.grad = None if skip else gg.to(dev)
+            b.grad = None if skip else gg.to(dev)
+        o1.step()
+        o2.step()
+    for a, b in zip(ours, ref):
+        assert torch.allclose(a.detach(), b.detach(), rtol=5e-7, atol=1e-8)
+    assert o1.state[ours[1]]["step"].item() == 3 and o1.state[ours[0]]["step"].item() == 4
+    # argument validation without a launch
+    assert _lib.load().pntf_adamw_multi(65, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-8,
+                                        0.0, 1, None) != 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 37, 300])
 def test_weight_grads_ragged_multi_env_vs_oracle(n):
     """Per-pair env ids in random order (not contiguous), ragged sizes; fp64 oracle."""

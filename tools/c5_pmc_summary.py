@@ -51,7 +51,8 @@ def main():
     simd_cycles = 1024 * avg_ns * 1e-9 * clock
     mfma = sq["SQ_INSTS_VALU_MFMA_MOPS_F32"]
     waves = lds["SQ_WAVES"]
-    tile_steps = mfma / (waves / 256) / 5120 * 1.0   # 5120 MFMAs per wave per tile-step
+    # 20 480 v_mfma_f32_4x4x1_16b_f32 per tile-step (both sweeps), whatever the wave count
+    tile_steps = mfma / 20480.0
     req_bytes = tcc["TCP_TCC_READ_REQ_sum"] * 128
     wc = sq["SQ_WAVE_CYCLES"]
     j = {
@@ -61,7 +62,7 @@ def main():
         "avg_duration_ns": avg_ns, "probe": probe,
         "effective_clock_GHz": clock / 1e9,
         "tile_steps_per_launch": tile_steps,
-        "tile_steps_check": "MFMA count / (5120 per wave per tile-step x 4 waves per tile)",
+        "tile_steps_check": "MFMA count / 20480 per tile-step (%d waves per tile)" % round(waves / 256),
         "weight_stream_bytes_per_launch_from_TCP_TCC_READ_REQ_x128": req_bytes,
         "weight_stream_bytes_expected": tile_steps * WEIGHT_BYTES_PER_TILE_STEP,
         "l2_hit_rate": tcc["TCC_HIT_sum"] / (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"]),

@@ -90,6 +90,34 @@ __device__ __forceinline__ f32x16 wload(WScratch sc, int t, int lane) {
   return v;
 }
 
+// ---------------------------------------------------------------- LDS σ tiles
+// The σ tiles the reverse sweep consumes at once when a phase starts — generator[-2]'s four
+// (the head step, right after the forward -> reverse drain) and the merge switch's four (the
+// merge Jacobian) — stay in LDS: 8 tiles x 4 KiB per wave, 128 KiB per workgroup (the kernel
+// uses no other LDS).  From the scratch slot each of those reloads waited out a whole HBM
+// round trip with nothing else in flight.  Layout as the scratch tiles: part q of a tile is
+// 1 KiB contiguous (lane-major f32x4), so ds_write_b128 / ds_read_b128 are conflict-free.
+typedef __attribute__((address_space(3))) f32x4 wlds_f4;
+constexpr int WL_G3 = 0, WL_S0 = 4, WL_TILES = 8;
+struct WLds {
+  wlds_f4* p;   // this wave's region, offset by the lane
+};
+__device__ __forceinline__ void lstore(WLds l, int t, const f32x16& v) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    l.p[(t * 4 + q) * 64] = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+}
+__device__ __forceinline__ f32x16 lload(WLds l, int t) {
+  f32x16 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 p = l.p[(t * 4 + q) * 64];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) v[4 * q + s] = p[s];
+  }
+  return v;
+}
+
 // ---------------------------------------------------------------- weight stream heads
 constexpr int WF = (OFF_WIDE + OFF_FWD) * 4;   // byte base of the forward wide fragments
 constexpr int WB = (OFF_WIDE + OFF_BWD) * 4;   // ... of the transposed ones
@@ -167,8 +195,9 @@ struct BiasCols {
   __device__ __forceinline__ float operator()(int ot) const { return v[ot / 4][ot % 4]; }
 };
 
-// forward Linear + softplus10: out = sp(A·in + b (+ out if RES)); σ10 saved when SAVE
-template <int OT_, int KT_, int NC_, bool RES, bool SAVE>
+// forward Linear + softplus10: out = sp(A·in + b (+ out if RES)); σ10 saved when SAVE (to
+// the scratch slot, or to LDS tiles sc0.. when IN_LDS)
+template <int OT_, int KT_, int NC_, bool RES, bool SAVE, bool IN_LDS = false>
 struct WFwdAct {
   static constexpr int OT = OT_, KT = KT_, NC = NC_;
   static constexpr bool DEFER = true;
@@ -176,6 +205,7 @@ struct WFwdAct {
   WScratch sc;
   int sc0, lane;
   BiasCols<OT_> bc;   // loaded by the caller one layer ahead
+  WLds wl;
   __device__ __forceinline__ void start() {}
   __device__ __forceinline__ void init(int ot, f32x16 (&acc)[NC]) {
 #pragma unroll
@@ -192,7 +222,8 @@ struct WFwdAct {
         g[r] = q.sg;
       }
       out[c * OT + ot] = h;
-      if (SAVE) wstore(sc, sc0 + c * OT + ot, lane, g);
+      if (SAVE && IN_LDS) lstore(wl, sc0 + c * OT + ot, g);
+      else if (SAVE) wstore(sc, sc0 + c * OT + ot, lane, g);
     }
   }
 };
@@ -267,7 +298,7 @@ __device__ __forceinline__ void wfourier_q(const PairIO& io, int kt, int h, f32x
 template <int DIM, bool GRAD, class AfterF>
 __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& io,
                                               f32x16 (&X)[8], f32x16 (&Y)[8], WScratch sc,
-                                              int compat, int lane, AfterF after) {
+                                              WLds wl, int compat, int lane, AfterF after) {
   const int h = lane >> 5;
   const float cm = compat ? 1.f : 0.f;
 
@@ -373,7 +404,7 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
       float rr = __builtin_amdgcn_rcpf(1.f + e);
       s0[r] = (d >= 0.f) ? rr : e * rr;
     }
-    if (GRAD) wstore(sc, WT_S0 + t, lane, s0);
+    if (GRAD) lstore(wl, WL_S0 + t, s0);
   }
 
   // ---- generator residual blocks (:246-249); X = u (8 tiles); gbc carries the next
@@ -395,7 +426,7 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
   }
   // ---- generator[-2] + act (:251-252) -> Y[0..3] (its bias columns: gbc's first 4 tiles)
   {
-    WFwdAct<4, 8, 1, false, GRAD> g3{Y, sc, WT_G3, lane, {}};
+    WFwdAct<4, 8, 1, false, GRAD, true> g3{Y, sc, WL_G3, lane, {}, wl};
     g3.bc.v[0] = gbc.v[0];
     wlayer<4, 8, 1, SITE_FWD_GEN, 4>(ring, W, WF + OFF_G3 * 4, X, lane, g3, NoPre{}, after);
   }
@@ -421,14 +452,14 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
 template <int DIM, class AfterF>
 __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& io, float tau,
                                               f32x16 (&X)[8], f32x16 (&Y)[8], WScratch sc,
-                                              int lane, float (&ds)[DIM], float (&dg)[DIM],
-                                              AfterF after) {
+                                              WLds wl, int lane, float (&ds)[DIM],
+                                              float (&dg)[DIM], AfterF after) {
   const int h = lane >> 5;
   // ---- head and generator[-2] (:592-613): Y[t] = d · g4w ⊙ σ10(y3)
   const float dd = 0.1f * tau * (1.f - tau);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    f32x16 s3 = wload(sc, WT_G3 + t, lane);
+    f32x16 s3 = lload(wl, WL_G3 + t);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       f32x4 w = bload(W, lane * 16, WHW + ((4 * t + u) * 64) * 16);
@@ -467,7 +498,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
   // ---- merge Jacobian (:620-627): X[0..3] = dzs, X[4..7] = dzg
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    f32x16 s0 = wload(sc, WT_S0 + t, lane);
+    f32x16 s0 = lload(wl, WL_S0 + t);
     f32x16 s1 = 1.f - s0;
     f32x16 dM = X[t], dm = X[4 + t];
     X[t] = s0 * dM + s1 * dm;
@@ -559,6 +590,10 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
   const WScratch sc =
       make_wscratch(GRAD ? a.ws + (int64_t)slot * WSCRATCH_FLOATS_PER_WAVE : nullptr);
   const Rsrc W = make_rsrc(a.P, PACKED_TOTAL * 4);
+  __shared__ f32x4 wsig[GRAD ? WAVES * WL_TILES * 4 * 64 : 1];
+  const WLds wl{(wlds_f4*)wsig +
+                (GRAD ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (WL_TILES * 4 * 64) + lane
+                      : 0)};
   Ring ring;
   ring_fill<4>(ring, W, lane * 16, WE0Head{});
   for (int tile = slot; tile < ntiles; tile += nslots) {
@@ -573,13 +608,13 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
     const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
     float tau;
     if constexpr (GRAD)
-      tau = wide_forward<DIM, true>(ring, W, io, X, Y, sc, a.compat, lane, wbwd_head());
+      tau = wide_forward<DIM, true>(ring, W, io, X, Y, sc, wl, a.compat, lane, wbwd_head());
     else
-      tau = wide_forward<DIM, false>(ring, W, io, X, Y, sc, a.compat, lane, WE0Head{});
+      tau = wide_forward<DIM, false>(ring, W, io, X, Y, sc, wl, a.compat, lane, WE0Head{});
     float ds[DIM], dg[DIM];
     if constexpr (GRAD) {
       drain_stores();
-      wide_backward<DIM>(ring, W, io, tau, X, Y, sc, lane, ds, dg, WE0Head{});
+      wide_backward<DIM>(ring, W, io, tau, X, Y, sc, wl, lane, ds, dg, WE0Head{});
     }
     const bool store = lane < 32 && pair < a.n;
     store_field<DIM, KIND>(a, pair, ok, store, tau, io, ds, dg);

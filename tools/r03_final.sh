@@ -32,5 +32,8 @@ echo C5_PMC_DONE
 cd "$R"
 bash tools/profile_round.sh
 echo PROFILED
+# stamp the headline PMC summary here, so the bench line below reports roofline.traffic
+python3 tools/prof_summary.py --tag r03 --pairs 1048576 > "$OUT/prof_summary.txt" 2>&1
+cp profiles/pmc_tau_grad.json "$OUT/pmc_tau_grad.json"
 timeout -k 10 600 python3 bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || { tail -20 "$OUT/bench_default.err"; exit 1; }
 cat "$OUT/bench_default.json"

@@ -91,8 +91,9 @@ def cpu_model():
 
 
 def cpu_baseline(sizes=(4096, 262144), reps=5):
-    """The reference's CPU op sequence (torch Linear/Softplus/logsumexp + autograd.grad with
-    create_graph, oracle/torch_ref.py, pinned to the reference by
+    """The reference's CPU call pattern (oracle/torch_ref.py: one NN.out(coords, B) +
+    Model.gradient autograd call per environment with that environment's (3, 128) B,
+    models/model_res_sigmoid_multi.py:186-190, 215-259, 890-896; pinned to the reference by
     tests/test_oracle_golden.py::test_torch_ref_cpu_baseline_vs_reference) on the same
     synthetic workload, as SURVEY.md §8(d) specifies: all host threads
     (torch.set_num_threads), one warm-up call, then the median of `reps` timed calls at each
@@ -120,11 +121,13 @@ def cpu_baseline(sizes=(4096, 262144), reps=5):
     big = str(max(sizes))
     return {"value": per_size[big]["pairs_per_s"], "unit": UNIT,
             "cores": torch.get_num_threads(), "kind": "port", "cpu_model": cpu_model(),
+            "pairs_per_s_per_core": per_size[big]["pairs_per_s"] / torch.get_num_threads(),
             "sizes": per_size,
             "sample": "median of %d reps after one warm-up at N = %s pairs (10 envs, per-pair "
                       "env id; `value` at N = %s) of the same synthetic workload through "
-                      "oracle/torch_ref.py (the reference's torch CPU op sequence: NN.out + "
-                      "Model.gradient autograd, create_graph=True), fp32, %.1f s timed"
+                      "oracle/torch_ref.py (the reference's torch CPU call pattern: one NN.out(coords, "
+                      "B) + Model.gradient autograd call, create_graph=True, per environment "
+                      "with its own (3,128) B), fp32, %.1f s timed"
                       % (reps, " and ".join(str(s) for s in sizes), big, total)}
 
 

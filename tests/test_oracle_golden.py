@@ -139,3 +139,28 @@ def test_torch_ref_cpu_baseline_vs_reference(W, name):
         t, d = ref.tau_grad(f["xp"], f["B"])
     assert rel_l2(t.numpy(), f["tau"].reshape(-1)) < TOL
     assert rel_l2(d.numpy(), f["dtau"]) < TOL
+    if "B_table" in f.files:
+        # the labelled per-pair gather form agrees too (it is only slower)
+        tg, dg = ref.tau_grad_gather(f["xp"], f["B_table"], f["env"])
+        assert rel_l2(tg.numpy(), f["tau"].reshape(-1)) < TOL
+        assert rel_l2(dg.numpy(), f["dtau"]) < TOL
+
+
+def test_torch_ref_per_env_calls_are_the_single_b_calls(W):
+    """The per-env split is exactly one single-B NN.out + Model.gradient call per env:
+    contiguous env blocks (the bench's layout) give bitwise the rows of those calls."""
+    from oracle.torch_ref import TorchRef, env_groups
+    ref = TorchRef(W)
+    xp = synth.make_pairs(300, 3, seed=2)
+    Bt = synth.make_B_table(3, 3)
+    env = synth.make_env_ids(300, 3)
+    groups = env_groups(env)
+    assert [g[0] for g in groups] == [0, 1, 2]
+    assert all(isinstance(g[1], slice) for g in groups)
+    t, d = ref.tau_grad(xp, Bt, env)
+    for e, rows in groups:
+        te, de = ref.tau_grad(xp[rows], Bt[e])
+        assert np.array_equal(t.numpy()[rows], te.numpy())
+        assert np.array_equal(d.numpy()[rows], de.numpy())
+    f = load("fwd_grad_env_d3.npz")              # interleaved ids -> gathered groups
+    assert all(not isinstance(g[1], slice) for g in env_groups(f["env"]))

@@ -205,7 +205,7 @@ int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, cons
                     int32_t n_env, float* phi, hipStream_t stream);
 
 /* Bias (+ residual) + act_laplace (:663-691, residual :744/:828) on GEMM output y (R, m, w),
- * w = 128|256, (ndir, nl) = (3|6, 1) or (6|12, 2): y's value plane += bias, every plane += res
+ * w = 128|256, (ndir, nl) = (3|6, 1), (6|12, 2) or (0, 0) (value plane only): y's value plane += bias, every plane += res
  * (R, m, w) when res is not NULL (y is kept as the tape); act != 0: h (R, m, w) = softplus10
  * Taylor rows.  act == 0 (Linear without activation, res must be NULL): bias only, h unused. */
 int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, const float* res,
@@ -223,6 +223,26 @@ int pntf_tt_act_bwd(int ndir, int nl, const float* y, float* g, int64_t m, int w
 int pntf_tt_merge_fwd(int dim, const float* z, int64_t n, float* u, hipStream_t stream);
 int pntf_tt_merge_bwd(int dim, const float* z, const float* gu, int64_t n, float* gz,
                       hipStream_t stream);
+
+/* ---- First-order (value-plane) tape: the weight gradient of a loss on NN.out's τ
+ * (models/model_res_sigmoid_multi.py:215-259, arm models/model_res_sigmoid.py:212-256: plain
+ * nn.Linear + autograd in the reference, so `net.out(x, B)[0].sum().backward()` fills every
+ * parameter's .grad).  The planes are R = 1 (value only, (ndir, nl) = (0, 0) in
+ * pntf_tt_act_fwd / pntf_tt_act_bwd / pntf_tt_linear_act); the GEMMs are pntf_tt_gemm's. */
+/* input_mapping (:186-190): phi (1, 2n, 256) = [sin | cos] of 2πxB (value plane of
+ * pntf_tt_fourier). */
+int pntf_tt_fourier_value(int dim, const float* xp, int64_t n, const float* Btab,
+                          const int32_t* env, int32_t n_env, float* phi, hipStream_t stream);
+/* Start/goal merge (:236-244) of the value plane: z (2n, 128) -> u (n, 256); adjoint
+ * (:620-627) gu (n, 256) -> gz (2n, 128). */
+int pntf_tt_merge_value_fwd(const float* z, int64_t n, float* u, hipStream_t stream);
+int pntf_tt_merge_value_bwd(const float* z, const float* gu, int64_t n, float* gz,
+                            hipStream_t stream);
+/* Head (:254-255): tau (n) = σ(0.1 (v·w4 + b4)) from generator[3]'s output v (n, 128) when tau
+ * is not NULL; with gtau (n) = dL/dτ (not NULL): gv (n, 128) = dL/dv, gw4 (128), gb4 (1). */
+int pntf_tt_head_tau(const float* v, const float* w4, const float* b4, int64_t n,
+                     const float* gtau, float* tau, float* gv, float* gw4, float* gb4,
+                     float* partial, hipStream_t stream);
 
 /* generator[4] + actout_laplace (:693-708) + Model.Loss (:897-946; arm = 1: the arm model's
  * square-root variant, models/model_res_sigmoid.py:869-935), forward and backward per pair:
@@ -254,7 +274,7 @@ const char* pntf_tt_gemm_last_error(void);
  * x (R, m, k) planes, W (n, k) the torch weight (y = x·Wᵀ), bias (n), res (R, m, n) or NULL
  * -> y (R, m, n) pre-activation (value plane + bias, every plane + res; kept as the tape) and,
  * when act != 0, h (R, m, n) the softplus10 Taylor rows.  R = 1 + ndir + nl with (ndir, nl) =
- * (3|6, 1) or (6|12, 2); k, n in {128, 256}; all pointers 16-byte aligned; `work` holds the
+ * (3|6, 1), (6|12, 2) or (0, 0); k, n in {128, 256}; all pointers 16-byte aligned; `work` holds the
  * packed weight (k*n floats).  act == 0 requires res == NULL (h unused).  schedule: 0 = AUTO
  * (the fused kernel when its 32-point blocks balance over the waves, else the two kernels),
  * 1 = always the fused kernel, 2 = always pntf_tt_gemm + pntf_tt_act_fwd; errors of either

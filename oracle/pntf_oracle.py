@@ -184,6 +184,56 @@ def tau_grad(params, xp, B, env=None, dim=3, dtype=np.float64, compat=False):
     return tau, dtau
 
 
+def tau_weight_grad(params, xp, B, wt, env=None, dim=3, dtype=np.float64):
+    """Gradient of Σ_p wt_p·τ_p w.r.t. every trained parameter and the coordinates — what
+    `(net.out(xp, B)[0][:, 0] * wt).sum().backward()` leaves in the reference's `.grad`
+    (models/model_res_sigmoid_multi.py:215-259 is plain nn.Linear + autograd).  Returns
+    (tau (n,), grads {key: array}, dcoords (n, 2dim)); encoder1.0 (never used, :160, :227)
+    gets no entry."""
+    tau, st = forward(params, xp, B, env, dim, dtype, keep=True)
+    p, n = st["p"], st["n"]
+    g = {}
+
+    def acc(name, gy, x):                                          # y = x W^T + b
+        g[name + ".weight"] = gy.T @ x
+        g[name + ".bias"] = gy.sum(axis=0)
+        return gy @ p[name + ".weight"]
+
+    enc, gen = st["enc"], st["gen"]
+    q = st["q"]
+    phi = np.concatenate([np.sin(q), np.cos(q)], axis=1)
+    h_in = [softplus10(enc["e0"]), softplus10(enc["blk"][0][1])]
+    h2 = softplus10(enc["blk"][1][1])
+    z = _lin(h2, p, "encoder.3")
+    u_in = [merge(z[:n], z[n:])[0]] + [softplus10(gen["blk"][i][1]) for i in (0, 1)]
+    u3 = softplus10(gen["blk"][2][1])
+    v = softplus10(gen["g3"])
+    t = tau[:, 0]
+    gy4 = (np.asarray(wt, dtype) * 0.1 * t * (1.0 - t))[:, None]   # d sigmoid(0.1 y)/dy
+    gv = acc("generator.4", gy4, v)
+    gu = acc("generator.3", gv * sig10(gen["g3"]), u3)
+    for i in (2, 1, 0):
+        y1, y2 = gen["blk"][i]
+        gy2 = gu * sig10(y2)
+        ga = acc("generator1.%d" % i, gy2, softplus10(y1))
+        gu = acc("generator.%d" % i, ga * sig10(y1), u_in[i]) + gy2
+    s0 = st["s0"]
+    s1 = 1.0 - s0
+    gM, gm = gu[:, :H], gu[:, H:]
+    gz = np.concatenate([s0 * gM + s1 * gm, s1 * gM + s0 * gm])
+    gh = acc("encoder.3", gz, h2)
+    for i in (2, 1):
+        y1, y2 = enc["blk"][i - 1]
+        gy2 = gh * sig10(y2)
+        ga = acc("encoder1.%d" % i, gy2, softplus10(y1))
+        gh = acc("encoder.%d" % i, ga * sig10(y1), h_in[i - 1]) + gy2
+    dphi = acc("encoder.0", gh * sig10(enc["e0"]), phi)
+    gq = dphi[:, :H] * np.cos(q) - dphi[:, H:] * np.sin(q)
+    w = st["w"]
+    dp = np.einsum("nf,ndf->nd", gq, np.concatenate([w, w])) if st["per"] else gq @ w.T
+    return t, g, np.concatenate([dp[:n], dp[n:]], axis=1)
+
+
 # ------------------------------------------------------------------ epilogues (A9/A10)
 
 

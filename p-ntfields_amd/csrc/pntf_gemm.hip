@@ -598,7 +598,7 @@ __global__ __launch_bounds__(256, 1) void panel_act_kernel(ActArgs g) {
   const int64_t stride = (int64_t)nwg * 4;
   int64_t blk = (int64_t)wg * 4 + w;
   if (blk >= nblk) return;   // wave-uniform; no barrier follows
-  const int R = g.R, ndir = g.ndir, GK = g.ndir / g.nl;
+  const int R = g.R, ndir = g.ndir, GK = g.nl ? g.ndir / g.nl : 1;
   const bool has_res = g.res != nullptr, act = g.act != 0;
   // plane at sequence position i: 0, then per group l its GK J planes and its L plane
   auto plane_of = [&](int i) {
@@ -1028,7 +1028,7 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
     }
     return PNTF_OK;
   }
-  if (ta && !tb && beta == 0.f && wgrad_shape(M, N) && wgrad_enabled() && lda == M &&
+  if (ta && !tb && beta == 0.f && K > 0 && wgrad_shape(M, N) && wgrad_enabled() && lda == M &&
       ldb == N && work && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 &&
       ((uintptr_t)work & 15) == 0) {
     // rows per split: a multiple of 128 (4 waves x two 16-row chunks); the buffer offsets are
@@ -1113,7 +1113,7 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
 int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const float* W,
                        int n, const float* bias, const float* res, float* y, float* h, int act,
                        int schedule, float* work, size_t work_floats, hipStream_t stream) {
-  const bool planes = (nl == 1 && (ndir == 3 || ndir == 6)) ||
+  const bool planes = (nl == 0 && ndir == 0) || (nl == 1 && (ndir == 3 || ndir == 6)) ||
                       (nl == 2 && (ndir == 6 || ndir == 12));
   const auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (!planes || m < 0 || !panel_shape(n, k) || (m > 0 && (!x || !W || !bias || !y || !work ||

@@ -70,8 +70,9 @@ __device__ __forceinline__ float softplus10(float y) {
 
 // ---------------------------------------------------------------- Φ planes (:199-213)
 // phi (2 + DIM, 2n, 256): point m < n is x_start of pair m, m >= n the x_goal of pair m - n;
-// planes [value | ∂x_d (DIM) | Σ_d ∂²x_d].
-template <int DIM>
+// planes [value | ∂x_d (DIM) | Σ_d ∂²x_d].  FULL = false: the value plane only (input_mapping
+// :186-190, the first-order tape of NN.out's weight gradient).
+template <int DIM, bool FULL = true>
 __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict__ xp, int64_t n,
                                   const float* __restrict__ Btab, const int32_t* __restrict__ env,
                                   int32_t n_env, float* __restrict__ phi) {
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict
     const int e = env ? env[p] : 0;
     float* o = phi + m * 256 + j;
     if (e < 0 || e >= n_env) {
-      for (int r = 0; r < 2 + DIM; ++r) o[r * plane] = o[r * plane + H] = NAN;
+      for (int r = 0; r < (FULL ? 2 + DIM : 1); ++r) o[r * plane] = o[r * plane + H] = NAN;
       continue;
     }
     const float* B = Btab + (int64_t)e * DIM * H + j;
@@ -100,6 +101,7 @@ __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict
     sincosf(q, &s, &c);
     o[0] = s;
     o[H] = c;
+    if (!FULL) continue;
 #pragma unroll
     for (int k = 0; k < DIM; ++k) {
       o[(1 + k) * plane] = w[k] * c;
@@ -127,7 +129,7 @@ template <int NDIR, int NL, bool ACT, bool RES>
 __global__ __launch_bounds__(256) void tt_act_fwd_kernel(float* __restrict__ y, float* __restrict__ h,
                                   const float* __restrict__ bias, const float* __restrict__ res,
                                   int64_t M, int W) {
-  constexpr int GK = NDIR / NL;
+  constexpr int GK = NL ? NDIR / NL : 0;
   const int64_t plane = M * W;
   for (int64_t i = 4 * (blockIdx.x * (int64_t)blockDim.x + threadIdx.x); i < plane;
        i += 4 * (int64_t)gridDim.x * blockDim.x) {
@@ -193,7 +195,7 @@ template <int NDIR, int NL, int W, bool ACT>
 __global__ __launch_bounds__(256) void tt_act_bwd_kernel(const float* __restrict__ y,
                                                          float* __restrict__ g, int64_t M,
                                                          float* __restrict__ partial) {
-  constexpr int TPR = W / 4, RB = 256 / TPR, GK = NDIR / NL;
+  constexpr int TPR = W / 4, RB = 256 / TPR, GK = NL ? NDIR / NL : 0;
   const int64_t plane = M * W;
   const int j = 4 * (threadIdx.x % TPR);
   f4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -348,11 +350,79 @@ __global__ __launch_bounds__(256) void tt_merge_bwd_kernel(const float* __restri
   }
 }
 
+// Value plane only (the first-order tape of NN.out, :236-244): z (2n, 128) -> u (n, 256) and
+// the adjoint gu (n, 256) -> gz (2n, 128) with s0 = σ(10 (zs - zg)) (:620-627).
+__global__ __launch_bounds__(256) void tt_merge_value_fwd_kernel(const float* __restrict__ z,
+                                                                 int64_t n, float* __restrict__ u) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / H;
+    const int j = (int)(i % H);
+    const float zs = z[p * H + j], zg = z[(n + p) * H + j];
+    const float lse = log1pf(expf(-SCALE * fabsf(zs - zg))) / SCALE;
+    u[p * 256 + j] = fmaxf(zs, zg) + lse;
+    u[p * 256 + j + H] = fminf(zs, zg) - lse;
+  }
+}
+
+__global__ __launch_bounds__(256) void tt_merge_value_bwd_kernel(const float* __restrict__ z,
+                                                                 const float* __restrict__ gu,
+                                                                 int64_t n, float* __restrict__ gz) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / H;
+    const int j = (int)(i % H);
+    const int64_t is = p * H + j, ig = (n + p) * H + j;
+    const float s0 = sig10(z[is] - z[ig]), s1 = 1.f - s0;
+    const float gM = gu[p * 256 + j], gm = gu[p * 256 + j + H];
+    gz[is] = gM * s0 + gm * s1;
+    gz[ig] = gM * s1 + gm * s0;
+  }
+}
+
 // ---------------------------------------------------------------- head + loss, fwd and bwd
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// τ head of the first-order tape, one wave per pair: τ = σ(0.1 (w4·v + b4)) (:254-255) from
+// generator[3]'s output v (n, 128).  With gtau (the incoming dL/dτ per pair): g = gtau·τ'
+// (τ' = 0.1 τ (1 - τ), :295), gv = g·w4 and per-block partials of g_w4 = Σ g v, g_b4 = Σ g.
+__global__ __launch_bounds__(256) void tt_head_tau_kernel(
+    const float* __restrict__ v, const float* __restrict__ w4, const float* __restrict__ b4,
+    int64_t n, const float* __restrict__ gtau, float* __restrict__ tau, float* __restrict__ gv,
+    float* __restrict__ partial) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float wa = w4[lane], wb = w4[lane + 64], bias = b4[0];
+  float gwa = 0.f, gwb = 0.f, gb = 0.f;
+  for (int64_t p = blockIdx.x * 4 + wave; p < n; p += (int64_t)gridDim.x * 4) {
+    const float* row = v + p * H;
+    const float va = row[lane], vb = row[lane + 64];
+    const float y = wave_sum(fmaf(va, wa, vb * wb)) + bias;
+    const float t = 1.f / (1.f + expf(-0.1f * y));
+    if (tau && lane == 0) tau[p] = t;
+    if (!gtau) continue;
+    const float g = gtau[p] * (0.1f * t * (1.f - t));
+    gb += g;
+    gwa = fmaf(g, va, gwa);
+    gwb = fmaf(g, vb, gwb);
+    gv[p * H + lane] = g * wa;
+    gv[p * H + lane + 64] = g * wb;
+  }
+  if (!gtau) return;   // grid-uniform
+  __shared__ float red[4][129];
+  red[wave][lane] = gwa;
+  red[wave][lane + 64] = gwb;
+  if (lane == 0) red[wave][128] = gb;
+  __syncthreads();
+  if (threadIdx.x < 129) {
+    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                    red[3][threadIdx.x];
+    if (threadIdx.x < 128) partial[blockIdx.x * 128 + threadIdx.x] = s;
+    else partial[(int64_t)gridDim.x * 128 + blockIdx.x] = s;
+  }
 }
 
 // One wave per pair.  v (R, n, 128) = generator[3]'s Taylor output, R = 3 + 2 DIM planes
@@ -555,7 +625,8 @@ int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, cons
 
 int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, const float* res,
                     int64_t m, int w, int act, hipStream_t stream) {
-  const bool shape = (nl == 1 && (ndir == 3 || ndir == 6)) || (nl == 2 && (ndir == 6 || ndir == 12));
+  const bool shape = (nl == 0 && ndir == 0) || (nl == 1 && (ndir == 3 || ndir == 6)) ||
+                     (nl == 2 && (ndir == 6 || ndir == 12));
   if (!shape || m < 0 || (w != 128 && w != 256) || (m > 0 && (!y || !bias || (act && !h))) ||
       (res && !act))
     return fail("pntf_tt_act_fwd: bad arguments");
@@ -568,7 +639,9 @@ int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, con
                                    h, bias, res, m, w);                                     \
   else hipLaunchKernelGGL((tt_act_fwd_kernel<N, L, false, false>), g, b, 0, stream, y, h, bias, \
                           res, m, w);
-  if (nl == 1) {
+  if (nl == 0) {
+    PNTF_ACT_FWD(0, 0)
+  } else if (nl == 1) {
     if (ndir == 3) { PNTF_ACT_FWD(3, 1) }
     else { PNTF_ACT_FWD(6, 1) }
   } else {
@@ -581,7 +654,8 @@ int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, con
 
 int pntf_tt_act_bwd(int ndir, int nl, const float* y, float* g, int64_t m, int w, int act,
                     float* gbias, int accumulate, float* partial, hipStream_t stream) {
-  const bool shape = (nl == 1 && (ndir == 3 || ndir == 6)) || (nl == 2 && (ndir == 6 || ndir == 12));
+  const bool shape = (nl == 0 && ndir == 0) || (nl == 1 && (ndir == 3 || ndir == 6)) ||
+                     (nl == 2 && (ndir == 6 || ndir == 12));
   if (!shape || m < 0 || (w != 128 && w != 256) || !gbias || !partial ||
       (m > 0 && (!g || (act && !y))))
     return fail("pntf_tt_act_bwd: bad arguments");
@@ -592,7 +666,10 @@ int pntf_tt_act_bwd(int ndir, int nl, const float* y, float* g, int64_t m, int w
                               partial);                                                     \
   else hipLaunchKernelGGL((tt_act_bwd_kernel<N, L, W, false>), gr, b, 0, stream, y, g, m, \
                           partial);
-  if (nl == 1) {   // encoder planes are 128 wide
+  if (nl == 0) {   // value plane only (the first-order tape)
+    if (w == 128) { PNTF_ACT_BWD(0, 0, 128) }
+    else { PNTF_ACT_BWD(0, 0, 256) }
+  } else if (nl == 1) {   // encoder planes are 128 wide
     if (w != 128) return fail("pntf_tt_act_bwd: encoder planes are 128 wide");
     if (ndir == 3) { PNTF_ACT_BWD(3, 1, 128) }
     else { PNTF_ACT_BWD(6, 1, 128) }
@@ -627,6 +704,60 @@ int pntf_tt_merge_bwd(int dim, const float* z, const float* gu, int64_t n, float
   if (dim == 3) hipLaunchKernelGGL((tt_merge_bwd_kernel<3>), g, b, 0, stream, z, gu, n, gz);
   else hipLaunchKernelGGL((tt_merge_bwd_kernel<6>), g, b, 0, stream, z, gu, n, gz);
   return check_launch("tt_merge_bwd_kernel");
+}
+
+int pntf_tt_fourier_value(int dim, const float* xp, int64_t n, const float* Btab,
+                          const int32_t* env, int32_t n_env, float* phi, hipStream_t stream) {
+  if ((dim != 3 && dim != 6) || n < 0 || n_env < 1 || (n > 0 && (!xp || !Btab || !phi)))
+    return fail("pntf_tt_fourier_value: bad arguments");
+  if (n == 0) return PNTF_OK;
+  const unsigned g = grid_1d(2 * n * H);
+  if (dim == 3)
+    hipLaunchKernelGGL((tt_fourier_kernel<3, false>), dim3(g), dim3(256), 0, stream, xp, n, Btab,
+                       env, n_env, phi);
+  else
+    hipLaunchKernelGGL((tt_fourier_kernel<6, false>), dim3(g), dim3(256), 0, stream, xp, n, Btab,
+                       env, n_env, phi);
+  return check_launch("tt_fourier_kernel<value>");
+}
+
+int pntf_tt_merge_value_fwd(const float* z, int64_t n, float* u, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!z || !u))) return fail("pntf_tt_merge_value_fwd: bad arguments");
+  if (n == 0) return PNTF_OK;
+  hipLaunchKernelGGL(tt_merge_value_fwd_kernel, dim3(grid_1d(n * H)), dim3(256), 0, stream, z, n,
+                     u);
+  return check_launch("tt_merge_value_fwd_kernel");
+}
+
+int pntf_tt_merge_value_bwd(const float* z, const float* gu, int64_t n, float* gz,
+                            hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!z || !gu || !gz))) return fail("pntf_tt_merge_value_bwd: bad arguments");
+  if (n == 0) return PNTF_OK;
+  hipLaunchKernelGGL(tt_merge_value_bwd_kernel, dim3(grid_1d(n * H)), dim3(256), 0, stream, z, gu,
+                     n, gz);
+  return check_launch("tt_merge_value_bwd_kernel");
+}
+
+int pntf_tt_head_tau(const float* v, const float* w4, const float* b4, int64_t n,
+                     const float* gtau, float* tau, float* gv, float* gw4, float* gb4,
+                     float* partial, hipStream_t stream) {
+  if (n < 0 || !w4 || !b4 || (n > 0 && !v) || (!gtau && !tau) ||
+      (gtau && (!gv || !gw4 || !gb4 || !partial)))
+    return fail("pntf_tt_head_tau: bad arguments");
+  const int nb = nb_for((n + 3) / 4);
+  if (n > 0)
+    hipLaunchKernelGGL(tt_head_tau_kernel, dim3(nb), dim3(256), 0, stream, v, w4, b4, n, gtau, tau,
+                       gv, partial);
+  if (gtau) {
+    if (n == 0) {   // an empty batch: zero gradients
+      hipMemsetAsync(gw4, 0, 128 * sizeof(float), stream);
+      hipMemsetAsync(gb4, 0, sizeof(float), stream);
+      return check_launch("pntf_tt_head_tau");
+    }
+    launch_reduce(partial, nb, 128, gw4, 0, stream);
+    launch_reduce(partial + (int64_t)nb * 128, nb, 1, gb4, 0, stream);
+  }
+  return check_launch("tt_head_tau_kernel");
 }
 
 int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const float* b4,

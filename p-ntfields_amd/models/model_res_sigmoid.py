@@ -12,7 +12,7 @@ import torch
 
 from pntf import ops
 from pntf import train as _train
-from pntf.net import PackedCache, TauFunction, build_layers
+from pntf.net import PackedCache, TauFunction, build_layers, weight_term
 from pntf.net import init_weights as _init_weights
 
 from .model_res_sigmoid_multi import (DDSigmoid_out, DSigmoid, DSigmoid_out, Sigmoid,  # noqa
@@ -85,8 +85,10 @@ class NN(torch.nn.Module):
 
     def out(self, coords):
         coords = coords.clone().detach().requires_grad_(True)
-        tau = TauFunction.apply(coords, self._B(coords.device), None, self.packed(), self.dim)
-        return tau, coords
+        Bt = self._B(coords.device)
+        tau = TauFunction.apply(coords, Bt, None, self.packed(), self.dim)
+        wt = weight_term(self, coords, Bt, None, self.dim)   # reference: autograd to the weights
+        return (tau if wt is None else tau + wt), coords
 
     def out_grad(self, coords):
         t, d = ops.tau_grad(self.packed(), coords, self._B(coords.device), None, self.dim,

@@ -7,7 +7,8 @@ md`, test/gib_plan.py:4, train/train_gib_multi.py:3); putting `p-ntfields_amd/` 
 return shapes and state-dict keys are the reference's:
 
     NN(device, dim)                              :131-175
-      .out(coords, B) -> (tau (N,1), coords)     :215-259   fused HIP forward (+ ∇τ if needed)
+      .out(coords, B) -> (tau (N,1), coords)     :215-259   fused HIP forward (+ ∇τ if needed;
+                                                            weight grads by the HIP value tape)
       .out_grad(coords, B) -> (tau, dtau, coords):303-400   exact ∇τ (HIP reverse sweep)
       .out_backgrad(coords, B) -> (...)          :402-647   HIP reverse sweep, quirk kept
       .forward(coords, B)                        :850-854
@@ -28,7 +29,7 @@ import torch
 
 from pntf import ops
 from pntf import train as _train
-from pntf.net import PackedCache, TauFunction, build_layers
+from pntf.net import PackedCache, TauFunction, build_layers, weight_term
 from pntf.net import init_weights as _init_weights
 
 
@@ -112,9 +113,10 @@ class NN(torch.nn.Module):
         """τ (N,1) and the fresh grad-leaf coords (:215-259).  `env` (N,) int picks rows of a
         per-env B table (E,dim,128); the reference passes a single (dim,128) B."""
         coords = coords.clone().detach().requires_grad_(True)
-        tau = TauFunction.apply(coords, _as_table(B, coords.device), env, self.packed(),
-                                self.dim)
-        return tau, coords
+        Bt = _as_table(B, coords.device)
+        tau = TauFunction.apply(coords, Bt, env, self.packed(), self.dim)
+        wt = weight_term(self, coords, Bt, env, self.dim)   # reference: autograd to the weights
+        return (tau if wt is None else tau + wt), coords
 
     def out_grad(self, coords, B, env=None):
         """(τ (N,1), ∇τ (N,2dim), coords) — forward-mode Jacobian in the reference (:303-400);

@@ -71,6 +71,14 @@ SIGNATURES = {
     "pntf_tt_merge_fwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _i64, _c_void_p, _c_void_p]),
     "pntf_tt_merge_bwd": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _i64, _c_void_p,
                                          _c_void_p]),
+    "pntf_tt_fourier_value": (ctypes.c_int, [ctypes.c_int, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                             _i32, _c_void_p, _c_void_p]),
+    "pntf_tt_merge_value_fwd": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _c_void_p]),
+    "pntf_tt_merge_value_bwd": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _c_void_p,
+                                               _c_void_p]),
+    "pntf_tt_head_tau": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                        _c_void_p]),
     "pntf_tt_head_loss": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _c_void_p,
                                          _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32,
                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

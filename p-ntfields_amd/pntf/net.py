@@ -87,3 +87,52 @@ class TauFunction(torch.autograd.Function):
     def backward(ctx, grad_tau):
         (d,) = ctx.saved_tensors
         return grad_tau * d, None, None, None, None
+
+
+class TauWeightFunction(torch.autograd.Function):
+    """The weight-gradient half of NN.out: a zero-valued term added to τ whose backward gives
+    every trained parameter the gradient of Σ gτ·τ, as the reference's nn.Linear + autograd
+    graph does (models/model_res_sigmoid_multi.py:215-259).  Forward computes nothing (τ
+    itself comes from TauFunction's fused kernel); backward runs the value-only Taylor tape
+    forward and its adjoint on the HIP GEMMs (pntf/train.py tau_weight_grad).  A backward
+    that asks only for coords (Model.gradient = autograd.grad(τ, coords)) never reaches this
+    node, so the planner / ∇τ path pays nothing for it."""
+
+    @staticmethod
+    def forward(ctx, coords, B, env, dim, keys, *params):
+        ctx.save_for_backward(coords, B, env, *params)
+        ctx.dim, ctx.keys = dim, keys
+        return torch.zeros((coords.shape[0], 1), dtype=torch.float32, device=coords.device)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g):
+        from . import train
+        coords, B, env, *params = ctx.saved_tensors
+        p = dict(zip(ctx.keys, params))
+        grads = {k: torch.empty_like(v) for k, v in p.items()}
+        Btab = B if B.dim() == 3 else B.unsqueeze(0)
+        train.tau_weight_grad(p, coords, Btab.contiguous(), env, ctx.dim,
+                              g.reshape(-1), grads)
+        return (None,) * 5 + tuple(grads[k] for k in ctx.keys)
+
+
+def weight_term(module, coords, B, env, dim):
+    """τ's weight-gradient term for NN.out (TauWeightFunction) when autograd records a graph
+    and any parameter requires grad; None otherwise."""
+    if not torch.is_grad_enabled():
+        return None
+    from . import train
+    sd = module.state_dict(keep_vars=True)
+    keys = [k for k in train.trained_keys() if sd[k].requires_grad]
+    if not keys:
+        return None
+    for k in keys:
+        ops._require_device(sd[k], k)
+        if sd[k].dtype != torch.float32 or not sd[k].is_contiguous():
+            raise ops.PntfError("parameter %s must be fp32 contiguous" % k)
+    if env is not None:
+        env = env.to(device=coords.device, dtype=torch.int32).contiguous()
+    x = coords.detach().to(torch.float32).contiguous()
+    return TauWeightFunction.apply(x, B.detach().contiguous(), env, dim, keys,
+                                   *[sd[k] for k in keys])

@@ -106,7 +106,9 @@ class _Tape:
 
     def planes(self, R):
         """(ndir, nl) of a Taylor tensor with R planes: (dim, 1) in the encoder, (2dim, 2)
-        after the merge (pntf_train.hip)."""
+        after the merge (pntf_train.hip); (0, 0) for the value-only tape of NN.out."""
+        if R == 1:
+            return (0, 0)
         return (self.dim, 1) if R == 2 + self.dim else (2 * self.dim, 2)
 
     def lin(self, x3, name, act=True, res=None):
@@ -176,6 +178,18 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
                                 float(gamma), float(scale), _vp(diff), _vp(g),
                                 _vp(grads["generator.4.weight"]), _vp(grads["generator.4.bias"]),
                                 _vp(part), s), "pntf_tt_head_loss")
+    def merge_bwd(g):
+        gz = torch.empty((Re, 2 * n, H), dtype=torch.float32, device=dev)
+        check(lib.pntf_tt_merge_bwd(dim, _vp(z), _vp(g), n, _vp(gz), s), "pntf_tt_merge_bwd")
+        return gz
+    _adjoint(tape, g, grads, part, merge_bwd)
+    return diff
+
+
+def _adjoint(tape, g, grads, part, merge_bwd):
+    """Walk the tape back from g = dL/d(generator[3] output planes): per Linear the act adjoint
+    (+ bias gradient), the weight gradient and the input gradient; merge_bwd(g) at the merge."""
+    lib, s, dev, params = tape.lib, tape.s, tape.dev, tape.p
     pending = []
     for name, x3, y, act, has_res in reversed(tape.ops):
         R, M, K = x3.shape
@@ -201,10 +215,55 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
             gemm(gx.view(R * M, K), g2, W, ta=False, tb=False)
         g = gx
         if name == "generator.0":
-            gz = torch.empty((Re, 2 * n, H), dtype=torch.float32, device=dev)
-            check(lib.pntf_tt_merge_bwd(dim, _vp(z), _vp(g), n, _vp(gz), s), "pntf_tt_merge_bwd")
-            g = gz
-    return diff
+            g = merge_bwd(g)
+
+
+def tau_weight_grad(params, xp, Btab, env, dim, gtau, grads):
+    """Into `grads` (key -> tensor shaped like the parameter): the gradient of Σ_p gtau_p·τ_p
+    w.r.t. every trained parameter, τ = NN.out(xp, B) (models/model_res_sigmoid_multi.py:
+    215-259; arm models/model_res_sigmoid.py:212-256) — what the reference's autograd leaves
+    in `.grad` after a backward through NN.out.  The value-only tape (R = 1): Fourier value
+    plane, per Linear one GEMM + the fused bias/residual/softplus kernel, the value merge,
+    the τ head with dL/dτ, then the same adjoint sweep as the Eikonal loss.  Returns τ (n,)."""
+    dev = xp.device
+    lib = _lib.load()
+    n = xp.shape[0]
+    tau = torch.empty(n, dtype=torch.float32, device=dev)
+    if n == 0:
+        for g in grads.values():
+            g.zero_()
+        return tau
+    tape = _Tape(params, dim, dev)
+    s = tape.s
+    phi = torch.empty((1, 2 * n, 2 * H), dtype=torch.float32, device=dev)
+    check(lib.pntf_tt_fourier_value(dim, _vp(xp), n, _vp(Btab), _vp(env), Btab.shape[0],
+                                    _vp(phi), s), "pntf_tt_fourier_value")
+    h = tape.lin(phi, "encoder.0")
+    for i in (1, 2):
+        a = tape.lin(h, "encoder.%d" % i)
+        h = tape.lin(a, "encoder1.%d" % i, res=h)
+    z = tape.lin(h, "encoder.3", act=False)
+    u = torch.empty((1, n, 2 * H), dtype=torch.float32, device=dev)
+    check(lib.pntf_tt_merge_value_fwd(_vp(z), n, _vp(u), s), "pntf_tt_merge_value_fwd")
+    for i in (0, 1, 2):
+        a = tape.lin(u, "generator.%d" % i)
+        u = tape.lin(a, "generator1.%d" % i, res=u)
+    v = tape.lin(u, "generator.3")
+    g = torch.empty_like(v)
+    part = _partial(dev)
+    gtau = gtau.detach().to(device=dev, dtype=torch.float32).contiguous()
+    check(lib.pntf_tt_head_tau(_vp(v), _vp(params["generator.4.weight"]),
+                               _vp(params["generator.4.bias"]), n, _vp(gtau), _vp(tau), _vp(g),
+                               _vp(grads["generator.4.weight"]), _vp(grads["generator.4.bias"]),
+                               _vp(part), s), "pntf_tt_head_tau")
+
+    def merge_bwd(gu):
+        gz = torch.empty((1, 2 * n, H), dtype=torch.float32, device=dev)
+        check(lib.pntf_tt_merge_value_bwd(_vp(z), _vp(gu), n, _vp(gz), s),
+              "pntf_tt_merge_value_bwd")
+        return gz
+    _adjoint(tape, g, grads, part, merge_bwd)
+    return tau
 
 
 def module_params(module):

@@ -1,7 +1,7 @@
 """Trained-weight (W2) goldens and reference-written checkpoints (build container only).
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_w2_goldens.py [--ref /root/reference]
-        [--steps 300] [--stage all|train|goldens|c5]
+        [--steps 400] [--stage all|train|goldens|c5]
 
 SURVEY.md §8c F5 / VERDICT r01 items 2 and 7.  The random-init goldens (make_goldens.py)
 leave softplus mostly unsaturated and plans short (22-25 steps).  This script, importing the
@@ -344,7 +344,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
-    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=400)   # the committed checkpoints: epoch 400
     ap.add_argument("--stage", default="all",
                     choices=["all", "train", "goldens", "c5", "train_grads"])
     args = ap.parse_args()

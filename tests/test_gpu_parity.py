@@ -335,6 +335,23 @@ def _elem_report(name, a, b):
                                                   max_rel(a, b, ELEM_FLOOR * scale))
 
 
+def per_pair_rel(a, b):
+    """Per-pair relative error: ‖a_p - b_p‖ / ‖b_p‖ over each pair's row (a scalar per pair
+    for τ, the 2·dim vector for ∇τ, the 2·dim Laplacian row for Δτ)."""
+    a = np.asarray(a, np.float64).reshape(len(a), -1)
+    b = np.asarray(b, np.float64).reshape(len(b), -1)
+    return np.linalg.norm(a - b, axis=1) / np.maximum(np.linalg.norm(b, axis=1), 1e-30)
+
+
+def north_star_per_pair(name, got, fp64, tol=1e-4):
+    """The north star's 1e-4 relative bound, held for EVERY pair of the sample against the
+    fp64 oracle (not only normwise over the batch)."""
+    r = per_pair_rel(got, fp64)
+    print("%s per-pair rel vs fp64: max %.2e (pair %d)" % (name, r.max(), int(r.argmax())))
+    assert r.max() < tol, "%s: pair %d per-pair rel %.3g >= %.1g" % (name, int(r.argmax()),
+                                                                      r.max(), tol)
+
+
 def test_residual_grad_agrees_with_reverse_sweep(packed, dev, W):
     """C3 at full size (BASELINE config 3: 1M pairs, 10 envs, Eikonal residual included):
     a 512-pair sample of τ, ∇τ, Δτ and the residual `diff` against the fp64 oracle
@@ -361,6 +378,16 @@ def test_residual_grad_agrees_with_reverse_sweep(packed, dev, W):
     close(got["dtau"], do)
     close(got["ltau"], lo)
     close(got["diff"], dfo)
+    # north star per pair: τ, ∇τ and the Laplacian row within 1e-4 of fp64 for every pair;
+    # diff = Σ_e (Ŝ/Y + Y/Ŝ) - 4 cancels (|diff| down to ~1e-3 beside summands of ~4), so it
+    # is held to 1e-4 of its summands' magnitude |diff| + 4 (fp32 itself gives 1.5e-4 of
+    # |diff| on this sample: tests measure)
+    north_star_per_pair("C3 tau", got["tau"], to[:, 0])
+    north_star_per_pair("C3 dtau", got["dtau"], do)
+    north_star_per_pair("C3 ltau", got["ltau"], lo)
+    dd = np.abs(got["diff"].astype(np.float64) - dfo) / (np.abs(dfo) + 4.0)
+    print("C3 diff |err|/(|diff|+4) max %.2e" % dd.max())
+    assert dd.max() < 1e-4
     # the 16-pair τ+∇τ kernel runs the same forward MFMA sequence: τ bit-identical
     t, d = ops.tau_grad(packed, xp, Bt, env, dim=3, schedule="wave_tile")
     assert torch.equal(out["tau"], t)
@@ -392,6 +419,18 @@ def test_headline_1m_sample_vs_fp64_oracle(packed, dev, W):
                                                   _elem_report("dtau", d[idx], do)))
     close(t[idx], to[:, 0], elem=1e-5)
     close(d[idx], do, elem=5e-4)
+    north_star_per_pair("headline tau", t[idx], to[:, 0])
+    north_star_per_pair("headline dtau", d[idx], do)
+    # componentwise (floored at 1 % of the largest |∇τ| component): no worse than the
+    # reference's own fp32 op sequence (oracle/torch_ref.py, the per-env NN.out +
+    # Model.gradient calls) against the same fp64 values — elementwise 1e-4 is not met by the
+    # fp32 reference itself (1.66e-4 on this sample, measured in the build container)
+    from oracle.torch_ref import TorchRef
+    tr, dr = TorchRef(W).tau_grad(xp_np[idx], Bt_np, env_np[idx])
+    floor = ELEM_FLOOR * np.abs(do).max()
+    e_hip, e_ref = max_rel(d[idx], do, floor), max_rel(dr.numpy(), do, floor)
+    print("headline dtau componentwise vs fp64: HIP %.2e, fp32 reference %.2e" % (e_hip, e_ref))
+    assert e_hip <= max(1e-4, 1.5 * e_ref)
 
 
 def test_device_sum_deterministic(dev):

@@ -233,32 +233,37 @@ def test_w2_planners_vs_reference(multi, arm, schedule):
 
 def c5_envelope_check(steps, fin, ref_iters, ref_final, f64_iters, f64_final, drift=None,
                       drift_paths=None, tol=1e-3):
-    """Query-by-query judgement of a C5 run.  Over 100-200 planner
-    steps through a trained field, fp32 summation-order differences are amplified on a few
-    trajectories; the fp64 oracle (plan_c5_w2_fp64.npz) says how far the fp32 reference itself
-    is from the exact plan on each query.  Every query must
-      * stop at an iteration count between the reference's and the fp64 plan's (inclusive),
-      * end within `tol` + 2·spread of the final state of a plan (reference or fp64) that
-        stopped at the same count, spread = |reference - fp64| on that query; on the queries
-        where the reference drifts (`drift`, whose full fp64 paths the fixture stores) a count
-        strictly between the two is judged against the fp64 state after that many steps.
-    Returns the per-query error and spread."""
+    """Query-by-query judgement of a C5 run.  Over 100-200
+    planner steps through a trained field, fp32 summation-order differences are amplified on
+    a few trajectories; the fp64 oracle (plan_c5_w2_fp64.npz) is the exact plan, and says how
+    far the fp32 reference itself is from it on each query.  Every query must
+      * stop at an iteration count between the reference's and the fp64 plan's (inclusive);
+      * end within `tol` of the reference's final state (when it stopped at the reference's
+        count), OR be no farther from the fp64 plan than the fp32 reference is: the distance
+        d_hip of its final state to the fp64 state after the same number of steps must not
+        exceed max(tol, d_ref), d_ref the reference's final-state distance to the fp64 state
+        after the reference's own number of steps.  (The fp64 state after k steps is the fp64
+        final state when k is the fp64 count; on the drifting queries, whose full fp64 paths
+        the fixture stores, it is known for every k.)
+    Returns (error vs the reference, d_hip, d_ref) per query (inf where undefined)."""
     lo, hi = np.minimum(ref_iters, f64_iters), np.maximum(ref_iters, f64_iters)
     bad = np.nonzero((steps < lo) | (steps > hi))[0]
     assert bad.size == 0, ("iteration counts outside the ref/fp64 envelope", bad.tolist(),
                            steps[bad].tolist(), ref_iters[bad].tolist(), f64_iters[bad].tolist())
-    spread = np.abs(ref_final - f64_final).max(1)
     inf = np.full(len(steps), np.inf)
     e_ref = np.where(steps == ref_iters, np.abs(fin - ref_final).max(1), inf)
-    e_64 = np.where(steps == f64_iters, np.abs(fin - f64_final).max(1), inf)
-    err = np.minimum(e_ref, e_64)
+    d_hip = np.where(steps == f64_iters, np.abs(fin - f64_final).max(1), inf)
+    d_ref = np.where(ref_iters == f64_iters, np.abs(ref_final - f64_final).max(1), inf)
     if drift is not None:
         for i, qi in enumerate(drift):
-            err[qi] = min(err[qi], np.abs(fin[qi] - drift_paths[i, steps[qi]]).max())
-    worst = np.nonzero(err > tol + 2 * spread)[0]
-    assert worst.size == 0, ("final states outside the envelope", worst.tolist(),
-                             err[worst].tolist(), spread[worst].tolist())
-    return err, spread
+            d_hip[qi] = np.abs(fin[qi] - drift_paths[i, steps[qi]]).max()
+            d_ref[qi] = np.abs(ref_final[qi] - drift_paths[i, ref_iters[qi]]).max()
+    ok = (e_ref <= tol) | (d_hip <= np.maximum(tol, d_ref))
+    worst = np.nonzero(~ok)[0]
+    assert worst.size == 0, ("final states neither within tol of the reference nor as close to "
+                             "fp64 as the reference", worst.tolist(), e_ref[worst].tolist(),
+                             d_hip[worst].tolist(), d_ref[worst].tolist())
+    return e_ref, d_hip, d_ref
 
 
 def test_c5_fp64_adjudication_fixture():
@@ -284,8 +289,8 @@ def test_w2_c5_1024_queries_vs_reference(arm):
     bench's planner call) vs 1024 independent reference batch-1 loops (test/arm_plan.py) at
     trained weights, where plans run 100-200 steps, judged query by query against the fp64
     oracle's plan (c5_envelope_check): every iteration count between the reference's and the
-    fp64 one, every final state within 1e-3 + 2·(reference - fp64 spread) of a plan that
-    stopped at the same count; 99 % of the iteration counts equal the reference's and 99 % of
+    fp64 one, every final state within 1e-3 of the reference's or no farther from the fp64
+    plan than the reference is; 99 % of the iteration counts equal the reference's and 99 % of
     the final states within 1e-3 of it; the 16 stored full paths within 1e-3."""
     dev = torch.device("cuda:0")
     c, f64 = load("plan_c5_w2.npz"), load("plan_c5_w2_fp64.npz")
@@ -296,15 +301,18 @@ def test_w2_c5_1024_queries_vs_reference(arm):
     fin = path[q, steps]
     dist = np.linalg.norm(fin[:, 6:] - fin[:, :6], axis=1)
     assert np.all((dist <= tol) | (steps > int(c["max_iter"])))
-    err, spread = c5_envelope_check(steps, fin, c["iters"], c["final"], f64["iters"],
-                                    f64["final"], f64["drift"], f64["drift_paths"])
+    e_ref, d_hip, d_ref = c5_envelope_check(steps, fin, c["iters"], c["final"], f64["iters"],
+                                            f64["final"], f64["drift"], f64["drift_paths"])
     d = f64["drift"]
-    print("C5 drifting queries %s: HIP steps %s, reference %s, fp64 %s; error %s, spread %s"
-          % (d.tolist(), steps[d].tolist(), c["iters"][d].tolist(), f64["iters"][d].tolist(),
-             np.round(err[d], 6).tolist(), np.round(spread[d], 6).tolist()))
+    print("C5 drifting queries (query: HIP steps / reference / fp64; HIP-vs-fp64, "
+          "reference-vs-fp64 distance at their own counts):")
+    for q in d:
+        print("  %4d: %3d / %3d / %3d   d_hip %.4g   d_ref %.4g   |HIP - ref| %s"
+              % (q, steps[q], c["iters"][q], f64["iters"][q], d_hip[q], d_ref[q],
+                 "%.4g" % e_ref[q] if np.isfinite(e_ref[q]) else "- (other count)"))
     same = steps == c["iters"]
     assert same.mean() >= 0.99, (int((~same).sum()), np.nonzero(~same)[0][:10].tolist())
-    assert np.quantile(err, 0.99) < 1e-3, float(np.quantile(err, 0.99))
+    assert np.quantile(np.minimum(e_ref, d_hip), 0.99) < 1e-3
     s16 = same[:16]
     assert np.abs(path[:16][s16] - c["paths16"][s16]).max() < 1e-3
 

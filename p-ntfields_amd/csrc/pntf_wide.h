@@ -49,8 +49,15 @@ struct WScratch {
 __device__ __forceinline__ WScratch make_wscratch(float* p) {
   return WScratch{make_rsrc(p, p ? WSCRATCH_FLOATS_PER_WAVE * 4 : 0)};
 }
+#ifdef PNTF_ABL_HOTLOAD   // diagnostics only: σ reloads from a 16 KiB region no store touches
+__device__ float pntf_abl_hot[4 * 1024];
+#endif
 // tile t = 4 KiB: part q (registers 4q..4q+3) of all lanes is 1 KiB contiguous
 __device__ __forceinline__ void wstore(WScratch sc, int t, int lane, const f32x16& v) {
+#ifdef PNTF_ABL_NOSTORE   // diagnostics only: the σ stores are dropped (wrong results)
+  asm volatile("" ::"v"(v[0]), "v"(v[5]), "v"(v[10]), "v"(v[15]));
+  return;
+#endif
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     f32x4 p{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
@@ -66,6 +73,10 @@ __device__ __forceinline__ f32x16 wload(WScratch sc, int t, int lane) {
 #endif
 #ifdef PNTF_ABL_L2LOAD    // diagnostics only: same loads, from a 16 KiB L2-resident region
   t &= 3;
+#endif
+#ifdef PNTF_ABL_HOTLOAD   // diagnostics only: same loads (nt, bypass L1) from an L2-hot region
+  sc.r = make_rsrc(pntf_abl_hot, 16384);
+  t = 0;
 #endif
 #ifdef PNTF_ABL_UNUSED    // diagnostics only: the loads issue, their data is not used
 #pragma unroll

@@ -277,11 +277,26 @@ const char* pntf_tt_gemm_last_error(void);
  * (3|6, 1), (6|12, 2) or (0, 0); k, n in {128, 256}; all pointers 16-byte aligned; `work` holds the
  * packed weight (k*n floats).  act == 0 requires res == NULL (h unused).  schedule: 0 = AUTO
  * (the fused kernel when its 32-point blocks balance over the waves, else the two kernels),
- * 1 = always the fused kernel, 2 = always pntf_tt_gemm + pntf_tt_act_fwd; errors of either
- * path are reported by pntf_tt_gemm_last_error / pntf_tt_last_error respectively. */
+ * 1 = always the fused kernel (one wave per 32-point block), 2 = always pntf_tt_gemm +
+ * pntf_tt_act_fwd, 3 = the fused kernel with the four waves of a workgroup sharing a block;
+ * errors of either path are reported by pntf_tt_gemm_last_error / pntf_tt_last_error. */
 int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const float* W,
                        int n, const float* bias, const float* res, float* y, float* h, int act,
                        int schedule, float* work, size_t work_floats, hipStream_t stream);
+
+/* The reverse of the same pair: the input gradient of one Linear with the previous layer's
+ * act_laplace adjoint (pntf_tt_act_bwd with act = 1) as its epilogue, in one kernel:
+ * gy (R, m, kc) the Linear's output-gradient planes, W (kc, nc) its torch weight, yprev (R, m,
+ * nc) the previous layer's pre-activation planes (its tape), res (R, m, nc) the residual
+ * branch's gradient or NULL -> out (R, m, nc) = the previous layer's dL/dy planes, i.e.
+ * act_bwd(gy·W + res), and gbias (nc) = their value plane summed over points (written, not
+ * accumulated).  out may alias res.  kc, nc in {128, 256}; (ndir, nl) as pntf_tt_act_fwd;
+ * 16-byte aligned pointers; `work` of pntf_tt_linear_bwd_work_floats(kc, nc) floats.  Errors
+ * via pntf_tt_gemm_last_error. */
+size_t pntf_tt_linear_bwd_work_floats(int kc, int nc);
+int pntf_tt_linear_bwd(int ndir, int nl, const float* gy, int64_t m, int kc, const float* W,
+                       int nc, const float* yprev, const float* res, float* out, float* gbias,
+                       float* work, size_t work_floats, hipStream_t stream);
 
 /* torch.optim.AdamW update of one parameter tensor (the reference's optimizer, :959-961):
  * p, grad, exp_avg, exp_avg_sq (n); `step` = the step count after this update (>= 1). */

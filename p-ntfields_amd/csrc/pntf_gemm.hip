@@ -702,6 +702,314 @@ __global__ __launch_bounds__(256, 1) void panel_act_kernel(ActArgs g) {
   }
 }
 
+// Cooperative form of the same fused Linear + act_laplace (schedule 3): the four waves of a
+// workgroup share one 32-point block, wave w computing out tile w (32 columns) of the
+// workgroup's 128-column group for every plane of the block, so the balance unit is a block
+// per WORKGROUP: at the reference batch 625 generator blocks over 128 workgroups per column
+// group (4.9 rounds, 98 % full) where panel_act_kernel gave 625 blocks to 512 waves (1.2
+// rounds: 61 %).  Per wave and plane: KC/2 MFMAs on one accumulator tile, its A panel (the
+// block's x rows of that plane, the same for the four waves: L1/L2 shared) loaded one plane
+// ahead, its fragments from LDS.  The act of a column needs only that column's σ(10 y₀) and
+// Σ J², so every wave keeps 16 of each and nothing crosses waves (no barrier in the loop).
+template <int KC, int NC>
+__global__ __launch_bounds__(256, 1) void panel_act_coop_kernel(ActArgs g) {
+  constexpr int QK = KC / 8, NG = NC / 128, FR = 4 * QK;
+  __shared__ f32x4 lw[FR * 64];
+  __shared__ f32x4 lb[32];   // the group's 128 biases
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int grp = 0, wg = blockIdx.x, nwg = gridDim.x;
+  if constexpr (NG == 2) {   // a block's two groups on one XCD (panel_lds_kernel)
+    const int x = blockIdx.x & 7, s = blockIdx.x >> 3;
+    grp = s & 1;
+    wg = (s >> 1) * 8 + x;
+    nwg = gridDim.x / 2;
+  }
+  {
+    const f32x4* src = g.P + (int64_t)grp * FR * 64;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < FR * 64; i += 256) lw[i] = src[i];
+    if (threadIdx.x < 32)
+      lb[threadIdx.x] = reinterpret_cast<const f32x4*>(g.bias)[grp * 32 + threadIdx.x];
+  }
+  __syncthreads();
+  const int64_t nblk = (g.M + 31) / 32;
+  int64_t blk = wg;
+  if (blk >= nblk) return;   // workgroup-uniform; no barrier follows
+  const int R = g.R, ndir = g.ndir, GK = g.nl ? g.ndir / g.nl : 1;
+  const bool has_res = g.res != nullptr, act = g.act != 0;
+  auto plane_of = [&](int i) {
+    if (i == 0) return 0;
+    const int l = (i - 1) / (GK + 1), k = (i - 1) % (GK + 1);
+    return k < GK ? 1 + l * GK + k : 1 + ndir + l;
+  };
+  auto win = [&](const float* base, int ld, int64_t b, int r) {
+    const int64_t rows = g.M - 32 * b;
+    return pg_rsrc(base + ((int64_t)r * g.M + 32 * b) * ld, (rows < 32 ? rows : 32) * ld * 4);
+  };
+  const int va = (j * KC + 4 * h) * 4, vc = (j * NC + 4 * h) * 4;
+  const int c0 = 128 * grp + 32 * w;   // the wave's 32 out columns
+  f32x4 x[QK];
+  {
+    const Rsrc ra = win(g.A, KC, blk, 0);
+#pragma unroll
+    for (int q = 0; q < QK; ++q) x[q] = pg_load(ra, va, 32 * q);
+  }
+  const f32x4* lf = lw + w * QK * 64 + lane;
+  f32x4 fr[2];
+  fr[0] = lf[0];
+  f32x4 s[4], jj[4];   // per feature of point j: σ(10 y₀), Σ J² of the current group
+  int i = 0;
+  for (;;) {
+    const int r = plane_of(i);
+    int ni = i + 1;
+    int64_t nb = blk;
+    if (ni == R) {
+      ni = 0;
+      nb = blk + nwg;
+    }
+    const bool more = nb < nblk;
+    const Rsrc rn = win(g.A, KC, more ? nb : blk, more ? plane_of(ni) : r);
+    const Rsrc ry = win(g.Y, NC, blk, r), rh = win(g.H, NC, blk, r);
+    const Rsrc rr = win(has_res ? g.res : g.Y, NC, blk, r);
+    const int kind = r == 0 ? 0 : r <= ndir ? ((r - 1) % GK == 0 ? 2 : 1) : 3;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    f32x4 cb[4];
+    pg_static_for<0, QK>([&](auto I) {
+      constexpr int q = decltype(I)::value, cur = q & 1;
+      if constexpr (q == QK - 4) {
+        if (has_res) {
+#pragma unroll
+          for (int Q = 0; Q < 4; ++Q) cb[Q] = pg_load(rr, vc, (c0 + 8 * Q) * 4);
+        }
+      }
+      constexpr int qn = (q + 1) % QK;
+      fr[cur ^ 1] = lf[qn * 64];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[cur][e], x[q][e], acc, 0, 0, 0);
+      if (more) x[q] = pg_load(rn, va, 32 * q);
+      if constexpr (q == QK - 1) {
+#pragma unroll
+        for (int Q = 0; Q < 4; ++Q) {
+          f32x4 v = {acc[4 * Q], acc[4 * Q + 1], acc[4 * Q + 2], acc[4 * Q + 3]};
+          if (kind == 0) v += lb[8 * w + 2 * Q + h];   // (acc + bias) + res, as tt_act_fwd
+          if (has_res) v += cb[Q];
+          const int off = (c0 + 8 * Q) * 4;
+          pg_store(ry, v, vc, off);
+          if (act) {
+            f32x4 hv;
+            if (kind == 0) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                s[Q][e] = pa_sig10(v[e]);
+                hv[e] = pa_softplus10(v[e]);
+              }
+            } else if (kind == 3) {
+              hv = 10.f * s[Q] * (1.f - s[Q]) * jj[Q] + v * s[Q];
+            } else {
+              hv = v * s[Q];
+              jj[Q] = kind == 2 ? v * v : jj[Q] + v * v;
+            }
+            pg_store(rh, hv, vc, off);
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (!more) break;
+    i = ni;
+    blk = nb;
+  }
+}
+
+// Input gradient of one Linear with the previous layer's act_laplace adjoint as its epilogue
+// (pntf_tt_linear_bwd; the reverse of a Linear of NN.out_laplace and the act before it, what
+// loss.backward() does at model_res_sigmoid_multi.py:1048 through :663-691): per plane
+//   g_h = gY·W (+ res, the residual branch's gradient),   then, with s = σ(10 y₀) of the
+//   previous layer's value plane, ds = 10 s (1 - s), dds = 10 ds (1 - 2 s):
+//   L_l:  g_yL = gL s                  acc₀ += gL (L ds)          (gL kept)
+//   J_k:  g_yJ = gJ s + 2 gL J ds      acc₀ += gJ J ds + gL dds J²
+//   value g_y₀ = g_h₀ s + acc₀         bias partial += g_y₀
+// (the formulas of tt_act_bwd_kernel, pntf_train.hip), so the g_h planes never round-trip
+// HBM between the GEMM and the act adjoint.  Same cooperative layout as
+// panel_act_coop_kernel: the four waves of a workgroup share a 32-point block, wave w owns out
+// tile w of the workgroup's 128-column group; a block's planes run L_l, its J planes, ..., the
+// value plane last.  The bias partials of a wave (its 32 columns, summed over its blocks and
+// then over the block's 32 points) go to partial[workgroup][NC] in a fixed order.
+struct BwdArgs {
+  const float* A;      // gY planes (R·M, KC)
+  const f32x4* P;      // packed W (panel_pack_kernel, tb = 0)
+  const float* Y;      // previous layer's pre-activation planes (R·M, NC)
+  const float* res;    // residual-branch gradient planes (R·M, NC) or null
+  float* G;            // out: g_y planes of the previous layer (R·M, NC); may alias res
+  float* partial;      // bias partials [workgroups per group][NC]
+  int64_t M;
+  int R, ndir, nl;
+};
+
+template <int KC, int NC>
+__global__ __launch_bounds__(256, 1) void panel_bwd_coop_kernel(BwdArgs g) {
+  constexpr int QK = KC / 8, NG = NC / 128, FR = 4 * QK;
+  __shared__ f32x4 lw[FR * 64];
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int grp = 0, wg = blockIdx.x, nwg = gridDim.x;
+  if constexpr (NG == 2) {
+    const int x = blockIdx.x & 7, s = blockIdx.x >> 3;
+    grp = s & 1;
+    wg = (s >> 1) * 8 + x;
+    nwg = gridDim.x / 2;
+  }
+  {
+    const f32x4* src = g.P + (int64_t)grp * FR * 64;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < FR * 64; i += 256) lw[i] = src[i];
+  }
+  __syncthreads();
+  const int c0 = 128 * grp + 32 * w;   // the wave's 32 out columns
+  f32x4 bsum[4];
+#pragma unroll
+  for (int Q = 0; Q < 4; ++Q) bsum[Q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nblk = (g.M + 31) / 32;
+  int64_t blk = wg;
+  if (blk < nblk) {
+    const int R = g.R, ndir = g.ndir, nl = g.nl, GK = nl ? ndir / nl : 1;
+    const bool has_res = g.res != nullptr;
+    // plane at sequence position i: per group l its L plane then its GK J planes; value last
+    auto plane_of = [&](int i) {
+      if (i == R - 1) return 0;
+      const int l = i / (GK + 1), k = i % (GK + 1);
+      return k == 0 ? 1 + ndir + l : 1 + l * GK + (k - 1);
+    };
+    auto win = [&](const float* base, int ld, int64_t b, int r) {
+      const int64_t rows = g.M - 32 * b;
+      return pg_rsrc(base + ((int64_t)r * g.M + 32 * b) * ld, (rows < 32 ? rows : 32) * ld * 4);
+    };
+    const int va = (j * KC + 4 * h) * 4, vc = (j * NC + 4 * h) * 4;
+    f32x4 x[QK];
+    {
+      const Rsrc ra = win(g.A, KC, blk, plane_of(0));
+#pragma unroll
+      for (int q = 0; q < QK; ++q) x[q] = pg_load(ra, va, 32 * q);
+    }
+    const f32x4* lf = lw + w * QK * 64 + lane;
+    f32x4 fr[2];
+    fr[0] = lf[0];
+    f32x4 s[4], gL[4], a0[4];
+    int i = 0;
+    for (;;) {
+      const int r = plane_of(i);
+      int ni = i + 1;
+      int64_t nb = blk;
+      if (ni == R) {
+        ni = 0;
+        nb = blk + nwg;
+      }
+      const bool more = nb < nblk;
+      const Rsrc rn = win(g.A, KC, more ? nb : blk, plane_of(more ? ni : i));
+      const Rsrc ry = win(g.Y, NC, blk, r), rg = win(g.G, NC, blk, r);
+      const Rsrc rr = win(has_res ? g.res : g.Y, NC, blk, r);
+      const Rsrc ry0 = win(g.Y, NC, blk, 0);
+      // 0 value, 1 J, 3 L
+      const int kind = r == 0 ? 0 : r <= ndir ? 1 : 3;
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      f32x4 cb[4], yt[4];
+      pg_static_for<0, QK>([&](auto I) {
+        constexpr int q = decltype(I)::value, cur = q & 1;
+        if constexpr (q == 0) {
+          if (i == 0) {   // block start: σ of the previous layer's value plane
+#pragma unroll
+            for (int Q = 0; Q < 4; ++Q) s[Q] = pg_load(ry0, vc, (c0 + 8 * Q) * 4);
+          }
+        }
+        if constexpr (q == QK - 4) {
+#pragma unroll
+          for (int Q = 0; Q < 4; ++Q) {
+            if (has_res) cb[Q] = pg_load(rr, vc, (c0 + 8 * Q) * 4);
+            if (kind != 0) yt[Q] = pg_load(ry, vc, (c0 + 8 * Q) * 4);
+          }
+        }
+        constexpr int qn = (q + 1) % QK;
+        fr[cur ^ 1] = lf[qn * 64];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[cur][e], x[q][e], acc, 0, 0, 0);
+        if (more) x[q] = pg_load(rn, va, 32 * q);
+        if constexpr (q == QK / 2) {
+          if (i == 0) {   // the loads above have had half a plane: σ from y₀, once per block
+#pragma unroll
+            for (int Q = 0; Q < 4; ++Q) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) s[Q][e] = pa_sig10(s[Q][e]);
+              a0[Q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
+        }
+        if constexpr (q == QK - 1) {
+#pragma unroll
+          for (int Q = 0; Q < 4; ++Q) {
+            f32x4 v = {acc[4 * Q], acc[4 * Q + 1], acc[4 * Q + 2], acc[4 * Q + 3]};
+            if (has_res) v += cb[Q];
+            const f32x4 sq = s[Q], ds = 10.f * sq * (1.f - sq);
+            f32x4 o;
+            if (kind == 3) {            // L_l: opens its group
+              gL[Q] = v;
+              o = v * sq;
+              a0[Q] += v * (yt[Q] * ds);
+            } else if (kind == 1) {     // J_k of the current group
+              const f32x4 J = yt[Q], dds = 10.f * ds * (1.f - 2.f * sq);
+              o = v * sq + 2.f * gL[Q] * J * ds;
+              a0[Q] += v * J * ds + gL[Q] * dds * (J * J);
+            } else {                    // value plane, last of the block
+              o = v * sq + a0[Q];
+              bsum[Q] += o;
+            }
+            pg_store(rg, o, vc, (c0 + 8 * Q) * 4);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      if (!more) break;
+      i = ni;
+      blk = nb;
+    }
+  }
+  // bias partials: sum the block's 32 points (lanes j of each half) for the wave's 16 columns
+  // per lane half, in a fixed butterfly order; lane (0, h) writes 16 columns
+#pragma unroll
+  for (int Q = 0; Q < 4; ++Q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = bsum[Q][e];
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      bsum[Q][e] = v;
+    }
+  if (j == 0) {   // row wg: the waves (and the groups' workgroups) fill disjoint columns
+#pragma unroll
+    for (int Q = 0; Q < 4; ++Q)
+      *reinterpret_cast<f32x4*>(g.partial + (int64_t)wg * NC + c0 + 8 * Q + 4 * h) = bsum[Q];
+  }
+}
+
+// gbias[c] = Σ_b partial[b][c] in row order (deterministic); one thread per column
+__global__ void colsum_kernel(const float* __restrict__ partial, int nb, int nc,
+                              float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  float a = 0.f, b = 0.f;
+  int r = 0;
+  for (; r + 1 < nb; r += 2) {
+    a += partial[(int64_t)r * nc + c];
+    b += partial[(int64_t)(r + 1) * nc + c];
+  }
+  if (r < nb) a += partial[(int64_t)r * nc + c];
+  out[c] = a + b;
+}
+
 // ---------------------------------------------------------------------------------------
 // Weight-gradient GEMM  gW (M x N) = gYᵀ (M x rows) · X (rows x N), M, N ∈ {128, 256}: the
 // reduction runs over every Taylor row of the tape (10⁵-10⁶), the output is one or a few
@@ -1122,7 +1430,7 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
     snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: bad arguments");
     return PNTF_ERR_ARG;
   }
-  if (schedule < 0 || schedule > 2) {
+  if (schedule < 0 || schedule > 3) {
     snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: unknown schedule");
     return PNTF_ERR_ARG;
   }
@@ -1139,7 +1447,8 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
   int64_t nwg = wgs < cap ? wgs : cap;
   if (ng == 2) nwg = (nwg + 7) / 8 * 8;
   const int64_t waves = 4 * nwg, rounds = (blocks + waves - 1) / waves;
-  const bool fused = schedule == 1 || (schedule == 0 && 10 * blocks >= 9 * rounds * waves);
+  const bool fused = schedule == 1 || schedule == 3 ||
+                     (schedule == 0 && 10 * blocks >= 9 * rounds * waves);
   if (!fused) {
     int st = pntf_tt_gemm(0, 1, R * m, n, k, x, k, W, k, y, n, 0.f, work, work_floats, stream);
     if (st) return st;
@@ -1149,6 +1458,22 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
   hipLaunchKernelGGL(panel_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0,
                      stream, W, (int64_t)k, 1, k, n, reinterpret_cast<f32x4*>(work));
   ActArgs a{x, reinterpret_cast<const f32x4*>(work), y, h, bias, res, m, R, ndir, nl, act};
+  if (schedule == 3) {
+    // cooperative blocks: one workgroup per CU and column group, each striding over blocks
+    int64_t cw = blocks < cap ? blocks : cap;
+    if (ng == 2) cw = (cw + 7) / 8 * 8;
+    const dim3 cg((unsigned)(cw * ng));
+    if (k == 128 && n == 128) hipLaunchKernelGGL((panel_act_coop_kernel<128, 128>), cg, dim3(256), 0, stream, a);
+    else if (k == 128) hipLaunchKernelGGL((panel_act_coop_kernel<128, 256>), cg, dim3(256), 0, stream, a);
+    else if (n == 128) hipLaunchKernelGGL((panel_act_coop_kernel<256, 128>), cg, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((panel_act_coop_kernel<256, 256>), cg, dim3(256), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: %s", hipGetErrorString(e));
+      return PNTF_ERR_HIP;
+    }
+    return PNTF_OK;
+  }
   // as the LDS panel GEMM: one workgroup per CU per column group (a multiple of 8 workgroups
   // per group for two groups); each wave strides over 32-point blocks
   const dim3 grid((unsigned)(nwg * ng));
@@ -1159,6 +1484,51 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(g_err, sizeof(g_err), "pntf_tt_linear_act: %s", hipGetErrorString(e));
+    return PNTF_ERR_HIP;
+  }
+  return PNTF_OK;
+}
+
+size_t pntf_tt_linear_bwd_work_floats(int kc, int nc) {
+  return (size_t)kc * nc + (size_t)num_cus() * nc;
+}
+
+int pntf_tt_linear_bwd(int ndir, int nl, const float* gy, int64_t m, int kc, const float* W,
+                       int nc, const float* yprev, const float* res, float* out, float* gbias,
+                       float* work, size_t work_floats, hipStream_t stream) {
+  const bool planes = (nl == 0 && ndir == 0) || (nl == 1 && (ndir == 3 || ndir == 6)) ||
+                      (nl == 2 && (ndir == 6 || ndir == 12));
+  const auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!planes || m < 0 || !panel_shape(nc, kc) || !gbias ||
+      (m > 0 && (!gy || !W || !yprev || !out || !work)) ||
+      work_floats < pntf_tt_linear_bwd_work_floats(kc, nc) || !al(gy) || !al(yprev) ||
+      !al(res) || !al(out) || !al(work)) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_linear_bwd: bad arguments");
+    return PNTF_ERR_ARG;
+  }
+  if (m == 0) {
+    hipMemsetAsync(gbias, 0, nc * sizeof(float), stream);
+    return PNTF_OK;
+  }
+  const int R = 1 + ndir + nl;
+  const int64_t nf = (int64_t)(nc / 32) * (kc / 8) * 64;
+  hipLaunchKernelGGL(panel_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0,
+                     stream, W, (int64_t)nc, 0, kc, nc, reinterpret_cast<f32x4*>(work));
+  float* partial = work + (size_t)kc * nc;
+  const int64_t blocks = (m + 31) / 32, ng = nc / 128, cap = num_cus() / ng;
+  int64_t cw = blocks < cap ? blocks : cap;
+  if (ng == 2) cw = (cw + 7) / 8 * 8;
+  BwdArgs a{gy, reinterpret_cast<const f32x4*>(work), yprev, res, out, partial, m, R, ndir, nl};
+  const dim3 cg((unsigned)(cw * ng));
+  if (kc == 128 && nc == 128) hipLaunchKernelGGL((panel_bwd_coop_kernel<128, 128>), cg, dim3(256), 0, stream, a);
+  else if (kc == 128) hipLaunchKernelGGL((panel_bwd_coop_kernel<128, 256>), cg, dim3(256), 0, stream, a);
+  else if (nc == 128) hipLaunchKernelGGL((panel_bwd_coop_kernel<256, 128>), cg, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((panel_bwd_coop_kernel<256, 256>), cg, dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(colsum_kernel, dim3((nc + 255) / 256), dim3(256), 0, stream, partial,
+                     (int)cw, nc, gbias);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "pntf_tt_linear_bwd: %s", hipGetErrorString(e));
     return PNTF_ERR_HIP;
   }
   return PNTF_OK;

@@ -53,7 +53,13 @@ constexpr int QRING_TAU = 64 / Q_WAVES;
 constexpr int QH = 64 / Q_WAVES;
 // groups of 16 out rows per wave of a layer with OUT rows
 constexpr int qg(int out) { return out / (16 * Q_WAVES); }
+// ring slot of layer L's first fragment: its position in the wave's stream mod the ring depth
+// (compile-time for every layer, so any ring depth that divides the per-step stream works)
+template <int L, int QR>
+constexpr int qslot() { return (q_layer_off(L) / 256) % QR; }
 constexpr int Q_NF_ALL = 2 * Q_NF_FWD;
+static_assert(Q_NF_ALL % QRING == 0 && Q_NF_FWD % QRING_TAU == 0,
+              "the ring depth must divide the per-step stream (its slots repeat every step)");
 constexpr int QBUF = 2 * 16 * 68;           // activation buffer: 2 columns x 16 lane rows x 68
 constexpr int QNSIG = 48;                   // saved σ10 slots per wave (64 floats each)
 constexpr int Q_RED = 3 * QBUF + Q_WAVES * QNSIG * 64;
@@ -303,7 +309,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[0] (:227); compat: the out_backgrad quirk (:435-438) stores σ10(softplus(y))
-  qlayer<2, 256, NF, qg(128), 0 % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
+  qlayer<2, 256, NF, qg(128), qslot<0, QR>(), QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       SpSig q = sp_sig(v[c] + pick(aux[0], g));
@@ -313,10 +319,10 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   });
   qsync();
   // ---- encoder residual blocks (:228-232): a: A -> B, b: B (+ A residual) -> A
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int la = 1 + 2 * blk, sa = QS_EBLK + 8 * blk;
-    qlayer<2, 128, NF, qg(128), 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  static_for<0, 2>([&](auto bb) {
+    constexpr int blk = decltype(bb)::value;
+    constexpr int la = 1 + 2 * blk, sa = QS_EBLK + 8 * blk;
+    qlayer<2, 128, NF, qg(128), qslot<la, QR>(), QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         SpSig q = sp_sig(v[c] + pick(aux[la], g));
@@ -325,7 +331,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
       }
     });
     qsync();
-    qlayer<2, 128, NF, qg(128), QH % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), qslot<la + 1, QR>(), QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -335,9 +341,9 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
       }
     });
     qsync();
-  }
+  });
   // ---- encoder[-1] (:234) and the smooth max / min merge (:236-244): u = [M | m] -> B
-  qlayer<2, 128, NF, qg(128), 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, qg(128), qslot<5, QR>(), QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const float zs = v[0] + pick(aux[5], g), zg = v[1] + pick(aux[5], g);
     const float d = zs - zg;
     const float e = exp_neg10abs(d);
@@ -352,27 +358,40 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   });
   qsync();
   // ---- generator residual blocks (:246-249): a: B -> A, b: A (+ B residual) -> B
-#pragma unroll 1
-  for (int i = 0; i < 3; ++i) {
+  // a generator block is 2 x 256 x 256 / Q_WAVES / 256 fragments; when the ring depth divides
+  // that, every block starts on the same slot and the loop stays rolled (code size)
+  auto gen_block = [&](int i, auto s0a, auto s0b) {
     const f32x4 ba = i == 0 ? aux[6] : i == 1 ? aux[8] : aux[10];
     const f32x4 bb = i == 0 ? aux[7] : i == 1 ? aux[9] : aux[11];
-    qlayer<1, 256, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, qg(256), decltype(s0a)::value, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       SpSig q = sp_sig(v[0] + pick(ba, g));
       *cx.at<256>(A, 0, g) = q.sp;
       if (GRAD) *cx.sig(QS_GBLK + 8 * i + g) = q.sg;
     });
     qsync();
-    qlayer<1, 256, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, qg(256), decltype(s0b)::value, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       SpSig q = sp_sig(v[0] + pick(bb, g) + *o);
       *o = q.sp;
       if (GRAD) *cx.sig(QS_GBLK + 8 * i + 4 + g) = q.sg;
     });
     qsync();
+  };
+  if constexpr ((2 * 256 * 256 / Q_WAVES / 256) % QR == 0) {
+#pragma unroll 1
+    for (int i = 0; i < 3; ++i)
+      gen_block(i, std::integral_constant<int, qslot<6, QR>()>{},
+                std::integral_constant<int, qslot<7, QR>()>{});
+  } else {
+    static_for<0, 3>([&](auto ii) {
+      constexpr int i = decltype(ii)::value;
+      gen_block(i, std::integral_constant<int, qslot<6 + 2 * i, QR>()>{},
+                std::integral_constant<int, qslot<7 + 2 * i, QR>()>{});
+    });
   }
   // ---- generator[-2] + act (:251-252) and the head generator[-1] (:254-255)
   float part[1] = {0.f};
-  qlayer<1, 256, NF, qg(128), QH % QR, QR, SOLO, NF == Q_NF_FWD>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+  qlayer<1, 256, NF, qg(128), qslot<12, QR>(), QR, SOLO, NF == Q_NF_FWD>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
     SpSig q = sp_sig(v[0] + pick(aux[12], g));
     part[0] = fmaf(pick(aux[13], g), q.sp, part[0]);
     if (GRAD) *cx.sig(QS_G3 + g) = q.sg;
@@ -396,24 +415,35 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   for (int g = 0; g < qg(128); ++g) *cx.at<128>(A, 0, g) = dd * pick(aux[13], g) * *cx.sig(QS_G3 + g);
   qsync();
   // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> B
-  qlayer<1, 128, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+  qlayer<1, 128, NF, qg(256), qslot<13, QR>(), QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
     *cx.at<256>(B, 0, g) = v[0] * *cx.sig(QS_GBLK + 16 + 4 + g);
   });
   qsync();
   // ---- generator blocks, reverse (:615-618): lb: B -> A, la: A (+ B residual) -> B
-#pragma unroll 1
-  for (int i = 2; i >= 0; --i) {
-    qlayer<1, 256, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+  auto gen_block_t = [&](int i, auto s0b, auto s0a) {
+    qlayer<1, 256, NF, qg(256), decltype(s0b)::value, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
       *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * i + g);
     });
     qsync();
     const int sb = QS_GBLK + 8 * (i - 1) + 4;   // σ10(y2) of block i - 1 (none for i = 0)
-    qlayer<1, 256, NF, qg(256), QH % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+    qlayer<1, 256, NF, qg(256), decltype(s0a)::value, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
       lds_f* o = cx.at<256>(B, 0, g);
       const float y = v[0] + *o;
       *o = i > 0 ? y * *cx.sig(sb + g) : y;
     });
     qsync();
+  };
+  if constexpr ((2 * 256 * 256 / Q_WAVES / 256) % QR == 0) {
+#pragma unroll 1
+    for (int i = 2; i >= 0; --i)
+      gen_block_t(i, std::integral_constant<int, qslot<14, QR>()>{},
+                  std::integral_constant<int, qslot<15, QR>()>{});
+  } else {
+    static_for<0, 3>([&](auto jj) {
+      constexpr int j = decltype(jj)::value;   // block i = 2 - j
+      gen_block_t(2 - j, std::integral_constant<int, qslot<14 + 2 * j, QR>()>{},
+                  std::integral_constant<int, qslot<15 + 2 * j, QR>()>{});
+    });
   }
   // ---- merge Jacobian (:620-627) on the wave's 128-row share: dz -> F (2 columns)
 #pragma unroll
@@ -426,22 +456,22 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1): F -> A
-  qlayer<2, 128, NF, qg(128), QH % QR, QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, qg(128), qslot<20, QR>(), QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) *cx.at<128>(A, c, g) = v[c] * *cx.sig(QS_EBLK + 12 + 2 * g + c);
   });
   qsync();
   // ---- encoder blocks, reverse (:633-636): b^T: A -> B (⊙ σ10(y1)), a^T: B (+ A) -> A
   // (⊙ σ10 of the layer below: block 0's y2, or encoder[0])
-#pragma unroll
-  for (int blk = 1; blk >= 0; --blk) {
-    const int sa = QS_EBLK + 8 * blk, sbelow = blk ? QS_EBLK + 4 : QS_E0;
-    qlayer<2, 128, NF, qg(128), 0 % QR, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  static_for<0, 2>([&](auto jj) {
+    constexpr int blk = 1 - decltype(jj)::value;
+    constexpr int sa = QS_EBLK + 8 * blk, sbelow = blk ? QS_EBLK + 4 : QS_E0;
+    qlayer<2, 128, NF, qg(128), qslot<21 + 2 * (1 - blk), QR>(), QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) *cx.at<128>(B, c, g) = v[c] * *cx.sig(sa + 2 * g + c);
     });
     qsync();
-    qlayer<2, 128, NF, qg(128), QH % QR, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), qslot<22 + 2 * (1 - blk), QR>(), QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -449,14 +479,14 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
       }
     });
     qsync();
-  }
+  });
   // ---- encoder[0]^T fused with the Fourier Jacobian (:639-645): the wave's 256/Q_WAVES
   // feature rows f (sin rows f < 128 in the first half of the waves, cos rows in the second),
   // both columns
   float acc[2 * DIM];
 #pragma unroll
   for (int i = 0; i < 2 * DIM; ++i) acc[i] = 0.f;
-  qlayer<2, 128, NF, qg(256), 0 % QR, QR, SOLO, true>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, qg(256), qslot<25, QR>(), QR, SOLO, true>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const int f = cx.w * (256 / Q_WAVES) + 16 * g + 4 * cx.og + cx.kb;
     const int fb = f & 127;
     float bw[DIM];

@@ -92,6 +92,11 @@ SIGNATURES = {
                                           _c_void_p, ctypes.c_int, _c_void_p, _c_void_p, _c_void_p,
                                           _c_void_p, ctypes.c_int, ctypes.c_int, _c_void_p,
                                           ctypes.c_size_t, _c_void_p]),
+    "pntf_tt_linear_bwd_work_floats": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    "pntf_tt_linear_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _i64, ctypes.c_int,
+                                          _c_void_p, ctypes.c_int, _c_void_p, _c_void_p,
+                                          _c_void_p, _c_void_p, _c_void_p, ctypes.c_size_t,
+                                          _c_void_p]),
     "pntf_adamw": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32,
                                   _f32, _f32, _f32, _i64, _c_void_p]),
     "pntf_adamw_multi": (ctypes.c_int, [ctypes.c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

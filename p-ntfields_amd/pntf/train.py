@@ -39,6 +39,9 @@ H = 128
 # 32-point blocks balance over the waves), 1 always fused, 2 always pntf_tt_gemm +
 # pntf_tt_act_fwd (the y planes round-trip HBM).  PNTF_TT_FUSED sets it (to compare).
 _LINEAR_ACT = int(os.environ.get("PNTF_TT_FUSED", "0"))
+# Input gradient + the previous layer's act adjoint in one kernel (pntf_tt_linear_bwd): 1, or
+# pntf_tt_gemm then pntf_tt_act_bwd: 0.  PNTF_TT_BWD sets it (to compare).
+_LINEAR_BWD = int(os.environ.get("PNTF_TT_BWD", "1"))
 _BLOCK_HEADS = ("encoder.1", "encoder.2", "generator.0", "generator.1", "generator.2")
 
 
@@ -188,16 +191,22 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
 
 def _adjoint(tape, g, grads, part, merge_bwd):
     """Walk the tape back from g = dL/d(generator[3] output planes): per Linear the act adjoint
-    (+ bias gradient), the weight gradient and the input gradient; merge_bwd(g) at the merge."""
+    (+ bias gradient), the weight gradient and the input gradient; merge_bwd(g) at the merge.
+    With _LINEAR_BWD the input gradient of a Linear and the act adjoint of the layer before it
+    run as one kernel (pntf_tt_linear_bwd) wherever that layer's output feeds this one directly
+    (not across the merge)."""
     lib, s, dev, params = tape.lib, tape.s, tape.dev, tape.p
     pending = []
-    for name, x3, y, act, has_res in reversed(tape.ops):
+    order = list(reversed(tape.ops))
+    fused_in = False          # this layer's act adjoint already ran in the previous kernel
+    for idx, (name, x3, y, act, has_res) in enumerate(order):
         R, M, K = x3.shape
         N = y.shape[2]
         ndir, nl = tape.planes(R)
-        check(lib.pntf_tt_act_bwd(ndir, nl, _vp(y), _vp(g), M, N, int(act),
-                                  _vp(grads[name + ".bias"]), 0, _vp(part), s),
-              "pntf_tt_act_bwd")
+        if not fused_in:
+            check(lib.pntf_tt_act_bwd(ndir, nl, _vp(y), _vp(g), M, N, int(act),
+                                      _vp(grads[name + ".bias"]), 0, _vp(part), s),
+                  "pntf_tt_act_bwd")
         g2 = g.view(R * M, N)
         weight_grad(g2, x3.view(R * M, K), grads[name + ".weight"])
         if name == "encoder.0":
@@ -205,10 +214,23 @@ def _adjoint(tape, g, grads, part, merge_bwd):
         if has_res:
             pending.append(g)
         W = params[name + ".weight"]
-        if name in _BLOCK_HEADS:
+        prev = order[idx + 1]
+        res = pending.pop() if name in _BLOCK_HEADS else None
+        fused_in = bool(_LINEAR_BWD) and name != "generator.0" and prev[3]
+        if fused_in:
+            # gx = act_bwd_prev(g·W (+ res)): in place into the residual branch's buffer
+            gx = res if res is not None else torch.empty((R, M, K), dtype=torch.float32,
+                                                         device=dev)
+            work = _work(dev, int(lib.pntf_tt_linear_bwd_work_floats(N, K)))
+            st = lib.pntf_tt_linear_bwd(ndir, nl, _vp(g), M, N, _vp(W), K, _vp(prev[2]),
+                                        _vp(res), _vp(gx), _vp(grads[prev[0] + ".bias"]),
+                                        _vp(work), work.numel(), s)
+            if st != 0:
+                raise PntfError("pntf_tt_linear_bwd: " + lib.pntf_tt_gemm_last_error().decode())
+        elif res is not None:
             # the block input also fed the residual add: accumulate into that branch's
             # gradient in place (beta = 1, no copy); it is not read again
-            gx = pending.pop()
+            gx = res
             gemm(gx.view(R * M, K), g2, W, ta=False, tb=False, beta=1.0)
         else:
             gx = torch.empty((R, M, K), dtype=torch.float32, device=dev)

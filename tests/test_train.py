@@ -450,6 +450,65 @@ def test_mfma_gemm_vs_fp64(ta, tb, M, N, K, beta):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", [1, 3])
+@pytest.mark.parametrize("dim", [3, 6])
+@pytest.mark.parametrize("n", [1, 77, 333])
+def test_fused_linear_act_ragged_vs_two_kernel(fused, dim, n, monkeypatch):
+    """Ragged point counts (a partial last 32-point block, n = 1 a single point) through the
+    fused Linear + act kernels — schedule 1 (one wave per block) and 3 (four waves per block)
+    — against the GEMM + act kernel pair (schedule 2): the Eikonal loss terms and every weight
+    gradient (dim and 2·dim planes, 128- and 256-wide layers, one and two column groups), and
+    the value-only tape of NN.out's weight gradient (R = 1); the fused side also runs the
+    input gradient + act adjoint kernel (pntf_tt_linear_bwd), the reference side the GEMM and
+    pntf_tt_act_bwd."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    W = weights()
+    params = {k: torch.from_numpy(W[k]).to(dev) for k in train.trained_keys()}
+    xp = synth.make_pairs(n, 3, seed=60 + n) if dim == 3 else synth.make_box_pairs(n, 6, seed=60 + n)
+    xp = torch.from_numpy(xp).to(dev)
+    yobs = torch.from_numpy(synth.make_speeds(n, seed=61)).to(dev)
+    Bt = torch.from_numpy(synth.make_B_table(2, dim)).to(dev)
+    env = torch.from_numpy(synth.make_env_ids(n, 2, contiguous=False, seed=n)).to(dev)
+    gtau = torch.linspace(-1.0, 1.0, n, device=dev)
+    out = {}
+    for sched in (fused, 2):
+        monkeypatch.setattr(train, "_LINEAR_ACT", sched)
+        monkeypatch.setattr(train, "_LINEAR_BWD", 1 if sched == fused else 0)
+        g = {k: torch.empty_like(v) for k, v in params.items()}
+        diff = train.loss_grad(params, xp, yobs, Bt, env, dim, 1e-3, 1.0 / n, dim == 6, g)
+        gv = {k: torch.empty_like(v) for k, v in params.items()}
+        tau = train.tau_weight_grad(params, xp, Bt, env, dim, gtau, gv)
+        out[sched] = (diff.clone(), g, tau.clone(), gv)
+    d1, g1, t1, v1 = out[fused]
+    d2, g2, t2, v2 = out[2]
+    assert torch.allclose(d1, d2, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(t1, t2, rtol=1e-6, atol=1e-7)
+    for k in params:
+        assert _rel(g1[k].cpu().numpy(), g2[k].cpu().numpy()) < 1e-5, k
+        assert _rel(v1[k].cpu().numpy(), v2[k].cpu().numpy()) < 1e-5, k
+
+
+@pytest.mark.gpu
+def test_tt_gemm_k0_with_work_buffer():
+    """pntf_tt_gemm with K = 0 on the weight-gradient shape (ta, beta 0, 128 x 128) and a
+    non-null work buffer writes C = 0 (the wgrad branch divided by zero)."""
+    import ctypes
+    from pntf import _lib
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    C = torch.full((128, 128), 7.0, device=dev)
+    A = torch.zeros(16, device=dev)
+    B = torch.zeros(16, device=dev)
+    work = torch.zeros(1 << 20, device=dev)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = lib.pntf_tt_gemm(1, 0, 128, 128, 0, vp(A), 128, vp(B), 128, vp(C), 128, 0.0, vp(work),
+                          work.numel(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert st == 0
+    assert torch.count_nonzero(C).item() == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,dim", CASES)
 def test_fused_linear_act_matches_two_kernel_path(name, dim, monkeypatch):
     """pntf_tt_linear_act (GEMM + bias + residual + act_laplace in one kernel) against the

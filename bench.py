@@ -438,6 +438,7 @@ def extras(packed, dev):
     out["c5_arm_plan_query_steps_per_s"] = float(steps.sum()) / (ms * 1e-3)
     out["c5_arm_plan_mean_steps"] = float(steps.mean())
     out["c5_arm_plan_max_steps"] = int(steps.max())
+    out["c5_arm_plan_handoffs"] = ops.plan_handoff_counts(dev)[1]   # 0 = no tail hand-off
     out["c5_arm_plan_1024q_wave_tile_ms"] = timeit(lambda: run_plan("wave_tile"), reps=2)
     out["c5_arm_plan_1024q_split_tile_ms"] = timeit(lambda: run_plan("split_tile"), reps=2)
     # the quad planner's C5 step time and its roofline: a step streams both weight directions

@@ -217,6 +217,18 @@ def plan(packed, xp0, Btab, env=None, dim=3, step=0.03, tol=0.06, max_iter=500,
     return path, steps
 
 
+def plan_handoff_counts(device):
+    """(queries the 4-query tiles counted done, queries handed to the SOLO launch) of the last
+    AUTO quad-tile plan on the current stream (pntf_plan_ex's tail counters at the start of
+    the workspace, pntf_quad.h "Tail hand-off").  A query that runs to max_iter without
+    converging is never counted done, so when more than CUs queries of a batch never converge
+    the hand-off does not fire (results are unaffected; the plan just keeps its MFMA tiles):
+    a zero second count shows that."""
+    ws = _ws_cache.get(device, 8)
+    c = ws[:8].view(torch.int32).cpu()
+    return int(c[0]), int(c[1])
+
+
 def eikonal_residual(packed, xp, Btab, env=None, dim=3, yobs=None, gamma=1e-3, want=("tau",
                      "dtau", "ltau", "diff")):
     """Taylor-mode τ, ∇τ, diagonal ∇²τ and the per-pair Eikonal residual of Model.Loss

@@ -359,36 +359,36 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   qsync();
   // ---- generator residual blocks (:246-249): a: B -> A, b: A (+ B residual) -> B
   // a generator block is 2 x 256 x 256 / Q_WAVES / 256 fragments; when the ring depth divides
-  // that, every block starts on the same slot and the loop stays rolled (code size)
-  auto gen_block = [&](int i, auto s0a, auto s0b) {
-    const f32x4 ba = i == 0 ? aux[6] : i == 1 ? aux[8] : aux[10];
-    const f32x4 bb = i == 0 ? aux[7] : i == 1 ? aux[9] : aux[11];
-    qlayer<1, 256, NF, qg(256), decltype(s0a)::value, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
-      SpSig q = sp_sig(v[0] + pick(ba, g));
-      *cx.at<256>(A, 0, g) = q.sp;
-      if (GRAD) *cx.sig(QS_GBLK + 8 * i + g) = q.sg;
-    });
-    qsync();
-    qlayer<1, 256, NF, qg(256), decltype(s0b)::value, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
-      lds_f* o = cx.at<256>(B, 0, g);
-      SpSig q = sp_sig(v[0] + pick(bb, g) + *o);
-      *o = q.sp;
-      if (GRAD) *cx.sig(QS_GBLK + 8 * i + 4 + g) = q.sg;
-    });
-    qsync();
-  };
+  // that, every block starts on the same slot and the loop stays rolled (code size).  (The
+  // body is a macro: as a lambda called with a runtime block index it put `aux` on the stack.)
+#define PNTF_QGEN_FWD(i, S0A, S0B)                                                                 \
+  {                                                                                                \
+    const f32x4 ba = (i) == 0 ? aux[6] : (i) == 1 ? aux[8] : aux[10];                              \
+    const f32x4 bb = (i) == 0 ? aux[7] : (i) == 1 ? aux[9] : aux[11];                              \
+    qlayer<1, 256, NF, qg(256), S0A, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {   \
+      SpSig q = sp_sig(v[0] + pick(ba, g));                                                        \
+      *cx.at<256>(A, 0, g) = q.sp;                                                                 \
+      if (GRAD) *cx.sig(QS_GBLK + 8 * (i) + g) = q.sg;                                             \
+    });                                                                                            \
+    qsync();                                                                                       \
+    qlayer<1, 256, NF, qg(256), S0B, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {   \
+      lds_f* o = cx.at<256>(B, 0, g);                                                              \
+      SpSig q = sp_sig(v[0] + pick(bb, g) + *o);                                                   \
+      *o = q.sp;                                                                                   \
+      if (GRAD) *cx.sig(QS_GBLK + 8 * (i) + 4 + g) = q.sg;                                         \
+    });                                                                                            \
+    qsync();                                                                                       \
+  }
   if constexpr ((2 * 256 * 256 / Q_WAVES / 256) % QR == 0) {
 #pragma unroll 1
-    for (int i = 0; i < 3; ++i)
-      gen_block(i, std::integral_constant<int, qslot<6, QR>()>{},
-                std::integral_constant<int, qslot<7, QR>()>{});
+    for (int i = 0; i < 3; ++i) PNTF_QGEN_FWD(i, (qslot<6, QR>()), (qslot<7, QR>()))
   } else {
     static_for<0, 3>([&](auto ii) {
       constexpr int i = decltype(ii)::value;
-      gen_block(i, std::integral_constant<int, qslot<6 + 2 * i, QR>()>{},
-                std::integral_constant<int, qslot<7 + 2 * i, QR>()>{});
+      PNTF_QGEN_FWD(i, (qslot<6 + 2 * i, QR>()), (qslot<7 + 2 * i, QR>()))
     });
   }
+#undef PNTF_QGEN_FWD
   // ---- generator[-2] + act (:251-252) and the head generator[-1] (:254-255)
   float part[1] = {0.f};
   qlayer<1, 256, NF, qg(128), qslot<12, QR>(), QR, SOLO, NF == Q_NF_FWD>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
@@ -420,31 +420,30 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   });
   qsync();
   // ---- generator blocks, reverse (:615-618): lb: B -> A, la: A (+ B residual) -> B
-  auto gen_block_t = [&](int i, auto s0b, auto s0a) {
-    qlayer<1, 256, NF, qg(256), decltype(s0b)::value, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
-      *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * i + g);
-    });
-    qsync();
-    const int sb = QS_GBLK + 8 * (i - 1) + 4;   // σ10(y2) of block i - 1 (none for i = 0)
-    qlayer<1, 256, NF, qg(256), decltype(s0a)::value, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
-      lds_f* o = cx.at<256>(B, 0, g);
-      const float y = v[0] + *o;
-      *o = i > 0 ? y * *cx.sig(sb + g) : y;
-    });
-    qsync();
-  };
+#define PNTF_QGEN_BWD(i, S0B, S0A)                                                                 \
+  {                                                                                                \
+    qlayer<1, 256, NF, qg(256), S0B, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {   \
+      *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * (i) + g);                                \
+    });                                                                                            \
+    qsync();                                                                                       \
+    const int sb = QS_GBLK + 8 * ((i) - 1) + 4;   /* σ10(y2) of block i - 1 (none for i = 0) */   \
+    qlayer<1, 256, NF, qg(256), S0A, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {   \
+      lds_f* o = cx.at<256>(B, 0, g);                                                              \
+      const float y = v[0] + *o;                                                                   \
+      *o = (i) > 0 ? y * *cx.sig(sb + g) : y;                                                      \
+    });                                                                                            \
+    qsync();                                                                                       \
+  }
   if constexpr ((2 * 256 * 256 / Q_WAVES / 256) % QR == 0) {
 #pragma unroll 1
-    for (int i = 2; i >= 0; --i)
-      gen_block_t(i, std::integral_constant<int, qslot<14, QR>()>{},
-                  std::integral_constant<int, qslot<15, QR>()>{});
+    for (int i = 2; i >= 0; --i) PNTF_QGEN_BWD(i, (qslot<14, QR>()), (qslot<15, QR>()))
   } else {
     static_for<0, 3>([&](auto jj) {
-      constexpr int j = decltype(jj)::value;   // block i = 2 - j
-      gen_block_t(2 - j, std::integral_constant<int, qslot<14 + 2 * j, QR>()>{},
-                  std::integral_constant<int, qslot<15 + 2 * j, QR>()>{});
+      constexpr int j = decltype(jj)::value, i = 2 - j;
+      PNTF_QGEN_BWD(i, (qslot<14 + 2 * j, QR>()), (qslot<15 + 2 * j, QR>()))
     });
   }
+#undef PNTF_QGEN_BWD
   // ---- merge Jacobian (:620-627) on the wave's 128-row share: dz -> F (2 columns)
 #pragma unroll
   for (int g = 0; g < qg(128); ++g) {

@@ -51,3 +51,21 @@ extern "C" int perf_set_stamps(unsigned long long* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(pntf::pntf_stamps), &p, sizeof(p)) == hipSuccess ? 0 : 1;
 }
 #endif
+
+#ifdef PERF_QUAD
+// C5-shaped planner launch of this build's quad kernels, the way pntf_plan_ex AUTO runs them:
+// the 4-query MFMA tiles with the tail hand-off, then the SOLO resume launch (tail = ws, 8 + 8q
+// bytes, zeroed by the caller).  dim 6, exact mode.
+extern "C" int perf_plan6(int grid, int cus, const float* P, const float* xp0, int64_t q,
+                          const float* Btab, float step, float tol, int max_iter, float* path,
+                          int32_t* steps, int32_t* tail, hipStream_t stream) {
+  using namespace pntf;
+  PlanArgs a{P, xp0, Btab, nullptr, q, 1, 0, step, tol, max_iter, path, steps, nullptr, tail,
+             (int32_t)cus};
+  dim3 b(64 * Q_WAVES);
+  hipLaunchKernelGGL((plan_quad_kernel<6, false>), dim3(grid), b, 0, stream, a);
+  if (tail)
+    hipLaunchKernelGGL((plan_quad_kernel<6, true>), dim3(q < cus ? q : cus), b, 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+#endif

@@ -336,8 +336,12 @@ def run(args):
     return 0
 
 
-def _timeit(fn, reps=5):
-    fn()
+def _timeit(fn, reps=5, warm=1):
+    """Mean time of `reps` back-to-back calls after `warm` untimed ones.  After any idle gap
+    the GPU's clocks ramp back over ~5 launches (profiles/r04_c2_launches.txt: 6.3 -> 5.2 ms
+    for the 262 144-pair kernel), so short kernels get a longer warm-up."""
+    for _ in range(warm):
+        fn()
     torch.cuda.synchronize()
     a = torch.cuda.Event(enable_timing=True)
     b = torch.cuda.Event(enable_timing=True)
@@ -394,11 +398,11 @@ def extras(packed, dev):
     n2 = 262144
     xp = torch.from_numpy(synth.make_pairs(n2, 3, seed=2)).to(dev)
     B = torch.from_numpy(synth.make_B(3, seed=1)).to(dev)
-    ms = timeit(lambda: ops.tau_grad(packed, xp, B, dim=3))
+    ms = timeit(lambda: ops.tau_grad(packed, xp, B, dim=3), reps=20, warm=8)
     out["c2_tau_grad_262144_pairs_per_s"] = n2 / (ms * 1e-3)
-    ms = timeit(lambda: ops.tau(packed, xp, B, dim=3))
+    ms = timeit(lambda: ops.tau(packed, xp, B, dim=3), reps=20, warm=8)
     out["c2_tau_only_262144_pairs_per_s"] = n2 / (ms * 1e-3)
-    ms = timeit(lambda: ops.path_velocity(packed, xp, B, dim=3))
+    ms = timeit(lambda: ops.path_velocity(packed, xp, B, dim=3), reps=20, warm=8)
     out["c2_path_velocity_262144_pairs_per_s"] = n2 / (ms * 1e-3)
     # the headline batch on the 16-pair kernel (pntf_field.h), for comparison with the wide one
     n1 = 1 << 20

@@ -779,7 +779,9 @@ __global__ __launch_bounds__(256, 1) void panel_act_coop_kernel(ActArgs g) {
     f32x4 cb[4];
     pg_static_for<0, QK>([&](auto I) {
       constexpr int q = decltype(I)::value, cur = q & 1;
-      if constexpr (q == QK - 4) {
+      // the residual planes come from HBM: load them a whole plane (QK·4 MFMAs) ahead of the
+      // epilogue (3 iterations of lead, as the one-wave kernel has, left ~2k cycles exposed)
+      if constexpr (q == 0) {
         if (has_res) {
 #pragma unroll
           for (int Q = 0; Q < 4; ++Q) cb[Q] = pg_load(rr, vc, (c0 + 8 * Q) * 4);
@@ -849,6 +851,9 @@ struct BwdArgs {
   int R, ndir, nl;
 };
 
+#ifndef PNTF_BWD_EARLY
+#define PNTF_BWD_EARLY (QK / 2)
+#endif
 template <int KC, int NC>
 __global__ __launch_bounds__(256, 1) void panel_bwd_coop_kernel(BwdArgs g) {
   constexpr int QK = KC / 8, NG = NC / 128, FR = 4 * QK;
@@ -926,7 +931,7 @@ __global__ __launch_bounds__(256, 1) void panel_bwd_coop_kernel(BwdArgs g) {
             for (int Q = 0; Q < 4; ++Q) s[Q] = pg_load(ry0, vc, (c0 + 8 * Q) * 4);
           }
         }
-        if constexpr (q == QK - 4) {
+        if constexpr (q == PNTF_BWD_EARLY) {   // HBM planes: half a plane of lead or more
 #pragma unroll
           for (int Q = 0; Q < 4; ++Q) {
             if (has_res) cb[Q] = pg_load(rr, vc, (c0 + 8 * Q) * 4);

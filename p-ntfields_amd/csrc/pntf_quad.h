@@ -57,6 +57,10 @@ constexpr int qg(int out) { return out / (16 * Q_WAVES); }
 // (compile-time for every layer, so any ring depth that divides the per-step stream works)
 template <int L, int QR>
 constexpr int qslot() { return (q_layer_off(L) / 256) % QR; }
+// layer L prefetches QR fragments ahead: past the end of the NF-fragment stream those loads
+// wrap to the next step's first layer (qfetch WRAP), which only the stream's last layers reach
+template <int L, int NF, int QR>
+constexpr bool qwrap() { return q_layer_off(L + 1) / 256 + QR > NF; }
 constexpr int Q_NF_ALL = 2 * Q_NF_FWD;
 static_assert(Q_NF_ALL % QRING == 0 && Q_NF_FWD % QRING_TAU == 0,
               "the ring depth must divide the per-step stream (its slots repeat every step)");
@@ -309,7 +313,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[0] (:227); compat: the out_backgrad quirk (:435-438) stores σ10(softplus(y))
-  qlayer<2, 256, NF, qg(128), qslot<0, QR>(), QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
+  qlayer<2, 256, NF, qg(128), qslot<0, QR>(), QR, SOLO, qwrap<0, NF, QR>()>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       SpSig q = sp_sig(v[c] + pick(aux[0], g));
@@ -322,7 +326,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   static_for<0, 2>([&](auto bb) {
     constexpr int blk = decltype(bb)::value;
     constexpr int la = 1 + 2 * blk, sa = QS_EBLK + 8 * blk;
-    qlayer<2, 128, NF, qg(128), qslot<la, QR>(), QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), qslot<la, QR>(), QR, SOLO, qwrap<la, NF, QR>()>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         SpSig q = sp_sig(v[c] + pick(aux[la], g));
@@ -331,7 +335,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
       }
     });
     qsync();
-    qlayer<2, 128, NF, qg(128), qslot<la + 1, QR>(), QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), qslot<la + 1, QR>(), QR, SOLO, qwrap<la + 1, NF, QR>()>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -343,7 +347,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
     qsync();
   });
   // ---- encoder[-1] (:234) and the smooth max / min merge (:236-244): u = [M | m] -> B
-  qlayer<2, 128, NF, qg(128), qslot<5, QR>(), QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, qg(128), qslot<5, QR>(), QR, SOLO, qwrap<5, NF, QR>()>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const float zs = v[0] + pick(aux[5], g), zg = v[1] + pick(aux[5], g);
     const float d = zs - zg;
     const float e = exp_neg10abs(d);
@@ -361,17 +365,17 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   // a generator block is 2 x 256 x 256 / Q_WAVES / 256 fragments; when the ring depth divides
   // that, every block starts on the same slot and the loop stays rolled (code size).  (The
   // body is a macro: as a lambda called with a runtime block index it put `aux` on the stack.)
-#define PNTF_QGEN_FWD(i, S0A, S0B)                                                                 \
+#define PNTF_QGEN_FWD(i, S0A, S0B, WA, WB)                                                                 \
   {                                                                                                \
     const f32x4 ba = (i) == 0 ? aux[6] : (i) == 1 ? aux[8] : aux[10];                              \
     const f32x4 bb = (i) == 0 ? aux[7] : (i) == 1 ? aux[9] : aux[11];                              \
-    qlayer<1, 256, NF, qg(256), S0A, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {   \
+    qlayer<1, 256, NF, qg(256), S0A, QR, SOLO, WA>(ring, W, cx, B, [&](int g, const float (&v)[1]) {   \
       SpSig q = sp_sig(v[0] + pick(ba, g));                                                        \
       *cx.at<256>(A, 0, g) = q.sp;                                                                 \
       if (GRAD) *cx.sig(QS_GBLK + 8 * (i) + g) = q.sg;                                             \
     });                                                                                            \
     qsync();                                                                                       \
-    qlayer<1, 256, NF, qg(256), S0B, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {   \
+    qlayer<1, 256, NF, qg(256), S0B, QR, SOLO, WB>(ring, W, cx, A, [&](int g, const float (&v)[1]) {   \
       lds_f* o = cx.at<256>(B, 0, g);                                                              \
       SpSig q = sp_sig(v[0] + pick(bb, g) + *o);                                                   \
       *o = q.sp;                                                                                   \
@@ -381,17 +385,19 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   }
   if constexpr ((2 * 256 * 256 / Q_WAVES / 256) % QR == 0) {
 #pragma unroll 1
-    for (int i = 0; i < 3; ++i) PNTF_QGEN_FWD(i, (qslot<6, QR>()), (qslot<7, QR>()))
+    for (int i = 0; i < 3; ++i)
+      PNTF_QGEN_FWD(i, (qslot<6, QR>()), (qslot<7, QR>()), (qwrap<10, NF, QR>()), (qwrap<11, NF, QR>()))
   } else {
     static_for<0, 3>([&](auto ii) {
       constexpr int i = decltype(ii)::value;
-      PNTF_QGEN_FWD(i, (qslot<6 + 2 * i, QR>()), (qslot<7 + 2 * i, QR>()))
+      PNTF_QGEN_FWD(i, (qslot<6 + 2 * i, QR>()), (qslot<7 + 2 * i, QR>()), (qwrap<6 + 2 * i, NF, QR>()),
+                    (qwrap<7 + 2 * i, NF, QR>()))
     });
   }
 #undef PNTF_QGEN_FWD
   // ---- generator[-2] + act (:251-252) and the head generator[-1] (:254-255)
   float part[1] = {0.f};
-  qlayer<1, 256, NF, qg(128), qslot<12, QR>(), QR, SOLO, NF == Q_NF_FWD>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
+  qlayer<1, 256, NF, qg(128), qslot<12, QR>(), QR, SOLO, qwrap<12, NF, QR>()>(ring, W, cx, B, [&](int g, const float (&v)[1]) {
     SpSig q = sp_sig(v[0] + pick(aux[12], g));
     part[0] = fmaf(pick(aux[13], g), q.sp, part[0]);
     if (GRAD) *cx.sig(QS_G3 + g) = q.sg;
@@ -415,19 +421,19 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   for (int g = 0; g < qg(128); ++g) *cx.at<128>(A, 0, g) = dd * pick(aux[13], g) * *cx.sig(QS_G3 + g);
   qsync();
   // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> B
-  qlayer<1, 128, NF, qg(256), qslot<13, QR>(), QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
+  qlayer<1, 128, NF, qg(256), qslot<13, QR>(), QR, SOLO, qwrap<13, NF, QR>()>(ring, W, cx, A, [&](int g, const float (&v)[1]) {
     *cx.at<256>(B, 0, g) = v[0] * *cx.sig(QS_GBLK + 16 + 4 + g);
   });
   qsync();
   // ---- generator blocks, reverse (:615-618): lb: B -> A, la: A (+ B residual) -> B
-#define PNTF_QGEN_BWD(i, S0B, S0A)                                                                 \
+#define PNTF_QGEN_BWD(i, S0B, S0A, WB, WA)                                                                 \
   {                                                                                                \
-    qlayer<1, 256, NF, qg(256), S0B, QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[1]) {   \
+    qlayer<1, 256, NF, qg(256), S0B, QR, SOLO, WB>(ring, W, cx, B, [&](int g, const float (&v)[1]) {   \
       *cx.at<256>(A, 0, g) = v[0] * *cx.sig(QS_GBLK + 8 * (i) + g);                                \
     });                                                                                            \
     qsync();                                                                                       \
     const int sb = QS_GBLK + 8 * ((i) - 1) + 4;   /* σ10(y2) of block i - 1 (none for i = 0) */   \
-    qlayer<1, 256, NF, qg(256), S0A, QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[1]) {   \
+    qlayer<1, 256, NF, qg(256), S0A, QR, SOLO, WA>(ring, W, cx, A, [&](int g, const float (&v)[1]) {   \
       lds_f* o = cx.at<256>(B, 0, g);                                                              \
       const float y = v[0] + *o;                                                                   \
       *o = (i) > 0 ? y * *cx.sig(sb + g) : y;                                                      \
@@ -436,11 +442,13 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   }
   if constexpr ((2 * 256 * 256 / Q_WAVES / 256) % QR == 0) {
 #pragma unroll 1
-    for (int i = 2; i >= 0; --i) PNTF_QGEN_BWD(i, (qslot<14, QR>()), (qslot<15, QR>()))
+    for (int i = 2; i >= 0; --i)
+      PNTF_QGEN_BWD(i, (qslot<14, QR>()), (qslot<15, QR>()), (qwrap<18, NF, QR>()), (qwrap<19, NF, QR>()))
   } else {
     static_for<0, 3>([&](auto jj) {
       constexpr int j = decltype(jj)::value, i = 2 - j;
-      PNTF_QGEN_BWD(i, (qslot<14 + 2 * j, QR>()), (qslot<15 + 2 * j, QR>()))
+      PNTF_QGEN_BWD(i, (qslot<14 + 2 * j, QR>()), (qslot<15 + 2 * j, QR>()), (qwrap<14 + 2 * j, NF, QR>()),
+                    (qwrap<15 + 2 * j, NF, QR>()))
     });
   }
 #undef PNTF_QGEN_BWD
@@ -455,7 +463,7 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   }
   qsync();
   // ---- encoder[-1]^T, then ⊙ σ10(y2 of encoder block 1): F -> A
-  qlayer<2, 128, NF, qg(128), qslot<20, QR>(), QR, SOLO>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, qg(128), qslot<20, QR>(), QR, SOLO, qwrap<20, NF, QR>()>(ring, W, cx, F, [&](int g, const float (&v)[2]) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) *cx.at<128>(A, c, g) = v[c] * *cx.sig(QS_EBLK + 12 + 2 * g + c);
   });
@@ -465,12 +473,12 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   static_for<0, 2>([&](auto jj) {
     constexpr int blk = 1 - decltype(jj)::value;
     constexpr int sa = QS_EBLK + 8 * blk, sbelow = blk ? QS_EBLK + 4 : QS_E0;
-    qlayer<2, 128, NF, qg(128), qslot<21 + 2 * (1 - blk), QR>(), QR, SOLO>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), qslot<21 + 2 * (1 - blk), QR>(), QR, SOLO, qwrap<21 + 2 * (1 - blk), NF, QR>()>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) *cx.at<128>(B, c, g) = v[c] * *cx.sig(sa + 2 * g + c);
     });
     qsync();
-    qlayer<2, 128, NF, qg(128), qslot<22 + 2 * (1 - blk), QR>(), QR, SOLO>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
+    qlayer<2, 128, NF, qg(128), qslot<22 + 2 * (1 - blk), QR>(), QR, SOLO, qwrap<22 + 2 * (1 - blk), NF, QR>()>(ring, W, cx, B, [&](int g, const float (&v)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         lds_f* o = cx.at<128>(A, c, g);
@@ -485,7 +493,7 @@ __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx
   float acc[2 * DIM];
 #pragma unroll
   for (int i = 0; i < 2 * DIM; ++i) acc[i] = 0.f;
-  qlayer<2, 128, NF, qg(256), qslot<25, QR>(), QR, SOLO, true>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
+  qlayer<2, 128, NF, qg(256), qslot<25, QR>(), QR, SOLO, qwrap<25, NF, QR>()>(ring, W, cx, A, [&](int g, const float (&v)[2]) {
     const int f = cx.w * (256 / Q_WAVES) + 16 * g + 4 * cx.og + cx.kb;
     const int fb = f & 127;
     float bw[DIM];

@@ -132,11 +132,16 @@ UNITS = (
     + [("plan_split_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_SPLIT"])
        for d in (3, 6)]
     # quad kernels (pntf_quad.h): 4-pair tiles, σ10 in LDS (no scratch slot)
+    # the ∇τ kernels run a 24-fragment weight ring per wave (PNTF_QRING; 16 in the SOLO units,
+    # where 24 spills): 192 KiB in flight per CU carries the stream across the layer barriers
+    # (quad tiles); the τ-only kernels stream the forward half with 8
     + [("quad_d%d_k%d" % (d, k), "pntf_kernels.hip",
-        ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_QUAD_FIELD"])
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_QUAD_FIELD"]
+        + (["-DPNTF_QRING=24"] if k in (1, 2, 3) else []))
        for d in (3, 6) for k in range(5)]
     + [("plan_quad_d%d" % d, "pntf_kernels.hip",
-        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=0"]) for d in (3, 6)]
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=0", "-DPNTF_QRING=24"])
+       for d in (3, 6)]
     # single-query planner (the reference's Q = 1 loop): quad layout, layers on the VALU
     + [("plan_quad_solo_d%d" % d, "pntf_kernels.hip",
         ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=1"]) for d in (3, 6)]

@@ -41,7 +41,7 @@ H = 128
 _LINEAR_ACT = int(os.environ.get("PNTF_TT_FUSED", "0"))
 # Input gradient + the previous layer's act adjoint in one kernel (pntf_tt_linear_bwd): 1, or
 # pntf_tt_gemm then pntf_tt_act_bwd: 0.  PNTF_TT_BWD sets it (to compare).
-_LINEAR_BWD = int(os.environ.get("PNTF_TT_BWD", "1"))
+_LINEAR_BWD = int(os.environ.get("PNTF_TT_BWD", "0"))
 _BLOCK_HEADS = ("encoder.1", "encoder.2", "generator.0", "generator.1", "generator.2")
 
 

@@ -276,7 +276,8 @@ const char* pntf_tt_gemm_last_error(void);
  * when act != 0, h (R, m, n) the softplus10 Taylor rows.  R = 1 + ndir + nl with (ndir, nl) =
  * (3|6, 1), (6|12, 2) or (0, 0); k, n in {128, 256}; all pointers 16-byte aligned; `work` holds the
  * packed weight (k*n floats).  act == 0 requires res == NULL (h unused).  schedule: 0 = AUTO
- * (the fused kernel when its 32-point blocks balance over the waves, else the two kernels),
+ * (the fused kernel when every wave gets >= 3 rounds of 32-point blocks that balance
+ * to >= 90 %, else the two kernels),
  * 1 = always the fused kernel (one wave per 32-point block), 2 = always pntf_tt_gemm +
  * pntf_tt_act_fwd, 3 = the fused kernel with the four waves of a workgroup sharing a block;
  * errors of either path are reported by pntf_tt_gemm_last_error / pntf_tt_last_error. */

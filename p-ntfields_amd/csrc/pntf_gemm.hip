@@ -1452,8 +1452,10 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
   int64_t nwg = wgs < cap ? wgs : cap;
   if (ng == 2) nwg = (nwg + 7) / 8 * 8;
   const int64_t waves = 4 * nwg, rounds = (blocks + waves - 1) / waves;
+  // (and only with several rounds per wave: at one round, generator[3] of the reference batch,
+  // the fused kernel measured 227 µs against 132 + 56 for the pair, profiles/r04_train_*)
   const bool fused = schedule == 1 || schedule == 3 ||
-                     (schedule == 0 && 10 * blocks >= 9 * rounds * waves);
+                     (schedule == 0 && rounds >= 3 && 10 * blocks >= 9 * rounds * waves);
   if (!fused) {
     int st = pntf_tt_gemm(0, 1, R * m, n, k, x, k, W, k, y, n, 0.f, work, work_floats, stream);
     if (st) return st;

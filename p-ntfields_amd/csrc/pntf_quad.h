@@ -47,6 +47,12 @@ constexpr int QCH = PNTF_Q_CHAINS;
 #define PNTF_QRING (128 / PNTF_QWAVES)
 #endif
 constexpr int QRING = PNTF_QRING;
+// the SOLO planner layers (one query per workgroup, VALU) hold their own accumulators beside
+// the ring: a unit may give them a different depth
+#ifndef PNTF_QRING_SOLO
+#define PNTF_QRING_SOLO PNTF_QRING
+#endif
+constexpr int QRING_SOLO = PNTF_QRING_SOLO;
 constexpr int QRING_TAU = 64 / Q_WAVES;
 // stream position (mod the ring) of a layer that follows a 128 x 128 one: the first ring slot
 // of every other encoder layer
@@ -62,7 +68,7 @@ constexpr int qslot() { return (q_layer_off(L) / 256) % QR; }
 template <int L, int NF, int QR>
 constexpr bool qwrap() { return q_layer_off(L + 1) / 256 + QR > NF; }
 constexpr int Q_NF_ALL = 2 * Q_NF_FWD;
-static_assert(Q_NF_ALL % QRING == 0 && Q_NF_FWD % QRING_TAU == 0,
+static_assert(Q_NF_ALL % QRING == 0 && Q_NF_ALL % QRING_SOLO == 0 && Q_NF_FWD % QRING_TAU == 0,
               "the ring depth must divide the per-step stream (its slots repeat every step)");
 constexpr int QBUF = 2 * 16 * 68;           // activation buffer: 2 columns x 16 lane rows x 68
 constexpr int QNSIG = 48;                   // saved σ10 slots per wave (64 floats each)
@@ -617,10 +623,11 @@ __global__ __launch_bounds__(64 * Q_WAVES, 1) void plan_quad_kernel(PlanArgs a) 
 #pragma unroll
   for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
   aux[13][2] = a.P[OFF_BIAS + B_G4B];
-  QRing<QRING> ring;
+  constexpr int QR = SOLO ? QRING_SOLO : QRING;
+  QRing<QR> ring;
   ring.off = 0;
 #pragma unroll
-  for (int s = 0; s < QRING; ++s) qfetch<Q_NF_ALL, QRING, false>(ring, W, cx.lane, s);
+  for (int s = 0; s < QR; ++s) qfetch<Q_NF_ALL, QR, false>(ring, W, cx.lane, s);
   const int cap = a.max_iter + 1;
   const int64_t rows = (int64_t)cap + 1;
   constexpr int TQ = SOLO ? 1 : QPAIRS;   // queries per tile
@@ -675,9 +682,9 @@ __global__ __launch_bounds__(64 * Q_WAVES, 1) void plan_quad_kernel(PlanArgs a) 
     for (; it < cap; ++it) {
       if (!__any(active) || yielded) break;
       const float tau =
-          quad_forward<DIM, true, Q_NF_ALL, QRING, SOLO>(ring, W, cx, io, aux, a.compat);
+          quad_forward<DIM, true, Q_NF_ALL, QR, SOLO>(ring, W, cx, io, aux, a.compat);
       float ds[DIM], dg[DIM], vs[DIM], vg[DIM];
-      quad_backward<DIM, Q_NF_ALL, QRING, SOLO>(ring, W, cx, io, tau, aux, ds, dg);
+      quad_backward<DIM, Q_NF_ALL, QR, SOLO>(ring, W, cx, io, tau, aux, ds, dg);
       path_velocity<DIM>(io.x, tau, ds, dg, vs, vg);
       bool converged = false;
       if (active) {

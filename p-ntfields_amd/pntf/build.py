@@ -132,7 +132,7 @@ UNITS = (
     + [("plan_split_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_SPLIT"])
        for d in (3, 6)]
     # quad kernels (pntf_quad.h): 4-pair tiles, σ10 in LDS (no scratch slot)
-    # the ∇τ kernels run a 24-fragment weight ring per wave (PNTF_QRING; 16 in the SOLO units,
+    # the ∇τ kernels run a 24-fragment weight ring per wave (PNTF_QRING; 22 in the SOLO units,
     # where 24 spills): 192 KiB in flight per CU carries the stream across the layer barriers
     # (quad tiles); the τ-only kernels stream the forward half with 8
     + [("quad_d%d_k%d" % (d, k), "pntf_kernels.hip",
@@ -144,7 +144,8 @@ UNITS = (
        for d in (3, 6)]
     # single-query planner (the reference's Q = 1 loop): quad layout, layers on the VALU
     + [("plan_quad_solo_d%d" % d, "pntf_kernels.hip",
-        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=1"]) for d in (3, 6)]
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=1", "-DPNTF_QRING=22"])
+       for d in (3, 6)]
     + [("residual_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_RESIDUAL"])
        for d in (3, 6)]
     + [("util", "pntf_kernels.hip", ["-DPNTF_UTIL"]), ("capi", "pntf_capi.hip", []),

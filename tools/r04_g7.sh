@@ -10,7 +10,7 @@ step() {
   return 0
 }
 step gpu_tests2 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
-step c5_ab 300 python -u tests/diag/c5_variants.py q16 q24k q16 q24k q16 q24k
+step c5_ab 300 python -u tests/diag/c5_variants.py q16 q24k q24s22 q16 q24k q24s22 q16 q24k q24s22
 step train_sched2 300 python -u tools/train_sched_probe.py 10
 step bench2 600 python -u bench.py --steps 20 --warmup 5
 tail -3 gpurun_out/r04_gpu_tests2.log

@@ -8,9 +8,12 @@
 // 1024-query plan (BASELINE C5) keeps only 64 CUs busy.  Here a tile is 4 pairs and the
 // matrix op is v_mfma_f32_4x4x1_16b_f32 (16 independent 4x4x1 blocks per instruction):
 //   * blocks b = 4·og + kb: og picks 4 of the instruction's 16 out rows, kb one of its 4 k;
-//     A lane l = W[r0 + 4·og + (l & 3)][k0 + kb], B lane l = act[k0 + kb][pair l & 3], so
-//     one instruction is 16 out rows x 4 k x 4 pairs and the accumulators hold one partial
-//     sum per k sub-block (kb), summed over the row (two DPP row_ror adds) after the layer;
+//     A lane l = W[r0 + 4·og + ((l + kb) & 3)][k0 + kb], B lane l = act[k0 + kb][pair l & 3],
+//     so one instruction is 16 out rows x 4 k x 4 pairs and accumulator element i of block
+//     (og, kb) holds row 4·og + ((i + kb) & 3) summed over k sub-block kb.  The rows are
+//     rotated by kb so that after the layer the four sub-blocks of a row sit on a diagonal:
+//     three DPP row_ror adds (a pairwise tree) leave row 4·og + kb in lane (og, kb, j), with
+//     no per-lane select (qring_sum);
 //   * the Q_WAVES = 8 waves of the workgroup (two per SIMD) own an eighth of every layer's
 //     out rows; after the sum each lane keeps one (row, pair) value ("compact": row
 //     r0 + 4·og + kb, pair l & 3), runs the epilogue on it and writes it to an LDS
@@ -54,6 +57,9 @@ constexpr int QRING = PNTF_QRING;
 #endif
 constexpr int QRING_SOLO = PNTF_QRING_SOLO;
 constexpr int QRING_TAU = 64 / Q_WAVES;
+#ifndef PNTF_QPIN
+#define PNTF_QPIN 1
+#endif
 // stream position (mod the ring) of a layer that follows a 128 x 128 one: the first ring slot
 // of every other encoder layer
 constexpr int QH = 64 / Q_WAVES;
@@ -92,12 +98,38 @@ __device__ __forceinline__ void qsync() {
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
-// v + v(lane rotated by N within its 16-lane row)
+// v of the lane CTRL selects (DPP row_ror:N = 0x120 + N: lane i of a 16-lane row reads
+// lane (i - N) mod 16; quad_perm 0x00: lane 4m reads lane 4m)
 template <int CTRL>
-__device__ __forceinline__ float dpp_add(float v) {
-  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-                                           0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                       0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
 }
+// Sum of the four k sub-blocks of a layer's rows.  t[i] of lane (og, kb, j) is row
+// (i + kb) & 3 over sub-block kb (pack_quad_kernel rotates the rows by kb), so S_k, row kb's
+// partial over sub-block k, is t[kb - k] of lane (og, k, j).  A pairwise tree in three DPP adds
+// with no per-lane select:
+//   B = t[0] + ror4(t[1])   in lane kb: S_kb + S_kb-1 of row kb
+//   A = t[2] + ror4(t[3])   in lane m: S_m + S_m-1 of row m + 2, so lane kb - 2 holds
+//                           S_kb-2 + S_kb-3 of row kb
+//   v = B + ror8(A)         (S_kb + S_kb-1) + (S_kb-2 + S_kb-3) = row kb, pair j
+// (the association of the unrotated layout's two full-row butterflies, so results do not
+// depend on the rotation).
+__device__ __forceinline__ float qring_sum(const f32x4& t) {
+  const float b = t[0] + dpp<0x124>(t[1]);
+  const float a = t[2] + dpp<0x124>(t[3]);
+  return b + dpp<0x128>(a);
+}
+// The same sum for a SOLO layer, whose lane (og, kb, r) holds one partial: row (r + kb) & 3
+// over sub-block kb, so S_k of row kb sits in lane (og, k, kb - k).  row_ror:3 reads lane
+// (k - 1, r + 1) from (k, r < 3): B = t + ror3(t) is S_kb + S_kb-1 in lane (kb, 0) and
+// S_kb-2 + S_kb-3 in lane (kb - 2, 2), six lanes below, so B + ror6(B) in lane (og, kb, 0) is
+// qring_sum's value bit for bit; a quad_perm broadcast gives it to the lane's other pair slots.
+__device__ __forceinline__ float qring_sum_solo(float t) {
+  const float b = t + dpp<0x123>(t);
+  return dpp<0x00>(b + dpp<0x126>(b));
+}
+
 // x ^ mask lane exchange inside 32-lane halves (ds_swizzle bit mode)
 template <int MASK>
 __device__ __forceinline__ float swz_xor(float v) {
@@ -155,6 +187,11 @@ __device__ __forceinline__ void qfetch(QRing<QR>& ring, Rsrc W, int lane, int sl
   ring.r[slot] = bload(W, lane * 16, ring.off);
 #endif
   ring.off += 1024;
+#if PNTF_QPIN
+  // keep the load where it is: under register pressure the scheduler otherwise sinks it to
+  // just before its use QR fragments later, and the ring drains to vmcnt(0) every layer
+  __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 
 // One layer: G groups of 16 out rows; per group IN/16 fragments of 4 k steps x NC columns;
@@ -182,7 +219,8 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
   if constexpr (SOLO) {
   // one active query in the tile (planner): the fragment runs on the VALU for that pair
   // (4 FMAs per column instead of 4 MFMAs of which 3 columns are idle); each lane's sum is
-  // row r0 + 4·og + (l & 3) over its k sub-block kb, and every pair slot carries the values
+  // row r0 + 4·og + ((l + kb) & 3) over its k sub-block kb, and every pair slot carries the
+  // values
   static_for<0, G>([&](auto gg) {
     constexpr int g = decltype(gg)::value;
     const lds_f* src0 = src;
@@ -207,19 +245,15 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
       qfetch<NF, QR, WRAP>(ring, W, cx.lane, slot);
     });
     float v[NC];
-    // the compact value of lane l is row r0 + 4·og + kb (the MFMA path's layout): take it
-    // from the lane of the same og whose row (l & 3) is this lane's kb AND whose k sub-block
-    // is kb too — there the dpp sums added the four sub-blocks in the order the MFMA path uses
-    // for row kb, so SOLO and the MFMA layers give bit-identical results (the planner's tail
-    // hand-off switches a query from one to the other mid-plan)
-    const int src_lane = (cx.lane & 0x30) | (cx.kb << 2) | cx.kb;
+    // the compact value of lane l is row r0 + 4·og + kb (the MFMA path's layout), summed in
+    // the MFMA path's order, so SOLO and the MFMA layers give bit-identical results (the
+    // planner's tail hand-off switches a query from one to the other mid-plan)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       float t = acc[c][0];
 #pragma unroll
       for (int h = 1; h < QCH; ++h) t += acc[c][h];
-      t = dpp_add<0x128>(dpp_add<0x124>(t));
-      v[c] = __shfl(t, src_lane);
+      v[c] = qring_sum_solo(t);
     }
     epi(g, v);
   });
@@ -254,15 +288,10 @@ __device__ __forceinline__ void qlayer(QRing<QR>& ring, Rsrc W, const QCx& cx, c
     float v[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      f32x4 s;
+      f32x4 t = acc[c][0];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float t = acc[c][0][i];
-#pragma unroll
-        for (int h = 1; h < QCH; ++h) t += acc[c][h][i];
-        s[i] = dpp_add<0x128>(dpp_add<0x124>(t));
-      }
-      v[c] = cx.kb == 0 ? s[0] : cx.kb == 1 ? s[1] : cx.kb == 2 ? s[2] : s[3];
+      for (int h = 1; h < QCH; ++h) t += acc[c][h];
+      v[c] = qring_sum(t);
     }
     epi(g, v);
   });
@@ -743,8 +772,8 @@ __global__ __launch_bounds__(64 * Q_WAVES, 1) void plan_quad_kernel(PlanArgs a) 
 #if defined(PNTF_UTIL)
 // ---------------------------------------------------------------- quad weight packing
 // Layer L of wave w: dst[w·Q_STREAM + r], r = ((g·IN/16 + q)·64 + l)·4 + e holds
-// A[w·OUT/4 + 16 g + 4 (l >> 4) + (l & 3)][16 q + 4 e + ((l >> 2) & 3)], A = M (dir 0) or
-// M^T (dir 1) of the rows x cols matrix M.
+// A[w·OUT/Q_WAVES + 16 g + 4 (l >> 4) + ((l + kb) & 3)][16 q + 4 e + kb], kb = (l >> 2) & 3,
+// A = M (dir 0) or M^T (dir 1) of the rows x cols matrix M (rows rotated by kb: qring_sum).
 __global__ void pack_quad_kernel(const float* __restrict__ src, int rows, int cols, int dir,
                                  float* __restrict__ dst) {
   const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -754,8 +783,9 @@ __global__ void pack_quad_kernel(const float* __restrict__ src, int rows, int co
   const int w = (int)(o / per), r = (int)(o % per);
   const int e = r & 3, l = (r >> 2) & 63, fq = r >> 8;
   const int g = fq / (IN / 16), q = fq % (IN / 16);
-  const int row = w * (OUT / Q_WAVES) + 16 * g + 4 * (l >> 4) + (l & 3);
-  const int k = 16 * q + 4 * e + ((l >> 2) & 3);
+  const int kb = (l >> 2) & 3;
+  const int row = w * (OUT / Q_WAVES) + 16 * g + 4 * (l >> 4) + ((l + kb) & 3);
+  const int k = 16 * q + 4 * e + kb;
   dst[(int64_t)w * Q_STREAM + r] = dir ? src[(int64_t)k * cols + row] : src[(int64_t)row * cols + k];
 }
 // Bias vectors: aux[w][L][l][g] = bias_L[w·OUT/4 + 16 g + 4 (l >> 4) + ((l >> 2) & 3)] for the

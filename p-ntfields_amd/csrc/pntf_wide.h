@@ -284,6 +284,27 @@ struct WBwd {
   }
 };
 
+// env B reads (Fourier projections and fold) and head-row reads, each behind a hook for
+// the tests/diag ablations (PNTF_ABL_NOBW / PNTF_ABL_NOHW: register stand-ins, wrong results)
+__device__ __forceinline__ f32x4 wbw_load(const float* p) {
+#ifdef PNTF_ABL_NOBW
+  float v = 1e-3f * (float)(reinterpret_cast<uintptr_t>(p) & 255);
+  asm volatile("v_mov_b32 %0, %0" : "+v"(v));
+  return f32x4{v, v + 1e-4f, v + 2e-4f, v + 3e-4f};
+#else
+  return ld4(p);
+#endif
+}
+__device__ __forceinline__ f32x4 whw_load(Rsrc W, int lane, int off) {
+#ifdef PNTF_ABL_NOHW
+  float v = 1e-3f * (float)((lane + off) & 255);
+  asm volatile("v_mov_b32 %0, %0" : "+v"(v));
+  return f32x4{v, v + 1e-4f, v + 2e-4f, v + 3e-4f};
+#else
+  return bload(W, lane * 16, off);
+#endif
+}
+
 // ---------------------------------------------------------------- Fourier projections
 // q[c][r] = x_c · 2πB[:, 32 kt + row(r, h)] for the lane's 16 feature rows of Fourier tile
 // kt, both points; the B rows come from the pair's environment (io.Bw, dim x 128).
@@ -295,7 +316,7 @@ __device__ __forceinline__ void wfourier_q(const PairIO& io, int kt, int h, f32x
   for (int d = 0; d < DIM; ++d)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 b = ld4(io.Bw + d * H + 32 * kt + 8 * u + 4 * h);
+      f32x4 b = wbw_load(io.Bw + d * H + 32 * kt + 8 * u + 4 * h);
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -447,7 +468,7 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 w = bload(W, lane * 16, WHW + ((4 * t + u) * 64) * 16);
+      f32x4 w = whw_load(W, lane, WHW + ((4 * t + u) * 64) * 16);
 #pragma unroll
       for (int s = 0; s < 4; ++s) part = fmaf(w[s], Y[t][4 * u + s], part);
     }
@@ -473,7 +494,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
     f32x16 s3 = lload(wl, WL_G3 + t);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 w = bload(W, lane * 16, WHW + ((4 * t + u) * 64) * 16);
+      f32x4 w = whw_load(W, lane, WHW + ((4 * t + u) * 64) * 16);
 #pragma unroll
       for (int s = 0; s < 4; ++s) Y[t][4 * u + s] = (dd * w[s]) * s3[4 * u + s];
     }
@@ -562,7 +583,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
           for (int u = 0; u < 4; ++u) {
             f32x4 bw[DIM];
 #pragma unroll
-            for (int d = 0; d < DIM; ++d) bw[d] = TWO_PI * ld4(io.Bw + d * H + 32 * o + 8 * u + 4 * h);
+            for (int d = 0; d < DIM; ++d) bw[d] = TWO_PI * wbw_load(io.Bw + d * H + 32 * o + 8 * u + 4 * h);
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll

@@ -112,6 +112,7 @@ SGPR_SPILL_FREE = re.compile(r"^wide_d\d_k[014]$")
 # measured when the unit was last changed; more than this fails the build.  None since the
 # quad kernels run 8 waves with a 16-fragment ring (the 4-wave SOLO planner kept 2 beside its
 # 32-fragment ring; with -DPNTF_QWAVES=4 raise these back to 2).
+QRING_MFMA, QRING_SOLO = 16, 22   # quad weight-ring depths (fragments per wave)
 VGPR_SPILL_ALLOWED = {"plan_quad_solo_d3": 0, "plan_quad_solo_d6": 0}
 
 UNITS = (
@@ -132,19 +133,19 @@ UNITS = (
     + [("plan_split_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_SPLIT"])
        for d in (3, 6)]
     # quad kernels (pntf_quad.h): 4-pair tiles, σ10 in LDS (no scratch slot)
-    # the ∇τ kernels run a 24-fragment weight ring per wave (PNTF_QRING; 22 in the SOLO units,
-    # where 24 spills): 192 KiB in flight per CU carries the stream across the layer barriers
-    # (quad tiles); the τ-only kernels stream the forward half with 8
+    # the ∇τ kernels run a QRING_MFMA-fragment weight ring per wave (PNTF_QRING; QRING_SOLO in
+    # the SOLO units), its loads pinned in program order (PNTF_QPIN, pntf_quad.h qfetch); the
+    # τ-only kernels stream the forward half with 8 (quad tiles)
     + [("quad_d%d_k%d" % (d, k), "pntf_kernels.hip",
         ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_QUAD_FIELD"]
-        + (["-DPNTF_QRING=24"] if k in (1, 2, 3) else []))
+        + (["-DPNTF_QRING=%d" % QRING_MFMA] if k in (1, 2, 3) else []))
        for d in (3, 6) for k in range(5)]
     + [("plan_quad_d%d" % d, "pntf_kernels.hip",
-        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=0", "-DPNTF_QRING=24"])
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=0", "-DPNTF_QRING=%d" % QRING_MFMA])
        for d in (3, 6)]
     # single-query planner (the reference's Q = 1 loop): quad layout, layers on the VALU
     + [("plan_quad_solo_d%d" % d, "pntf_kernels.hip",
-        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=1", "-DPNTF_QRING=22"])
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_PLAN_QUAD", "-DPNTF_QSOLO=1", "-DPNTF_QRING=%d" % QRING_SOLO])
        for d in (3, 6)]
     + [("residual_d%d" % d, "pntf_kernels.hip", ["-DPNTF_DIM=%d" % d, "-DPNTF_RESIDUAL"])
        for d in (3, 6)]

@@ -63,8 +63,11 @@ def main(names):
                       V(path), V(steps), V(tail), ctypes.c_void_p(stream)) == 0
         ms = timed(run)
         same = torch.equal(path, p0) and torch.equal(steps, s0)
-        print("%-10s  %.3f ms  handoffs %d  bitwise equal to shipped: %s" % (
-            name, ms, int(tail[1].item()), same), flush=True)
+        ok = torch.isfinite(path) & torch.isfinite(p0)
+        print("%-10s  %.3f ms  handoffs %d  bitwise equal to shipped: %s  max steps %d  "
+              "steps equal %d/%d  max |dpath| %.3g" % (
+                  name, ms, int(tail[1].item()), same, int(steps.max()),
+                  int((steps == s0).sum()), q, float((path - p0)[ok].abs().max())), flush=True)
 
 
 if __name__ == "__main__":

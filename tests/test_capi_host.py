@@ -171,37 +171,46 @@ def test_wide_pack_layout_feeds_32x32x2_fragments():
         assert frag[ot, kt, u, 32 * h + i, s] == W[32 * ot + i, 32 * kt + row(r, h)]
 
 
-def _pack_quad_numpy(W, dir_):
-    """Restatement of pack_quad_kernel (pntf_quad.h): the 4 wave streams of one layer,
-    shape (wave, groups, IN/16, 64 lanes, 4)."""
+def _pack_quad_numpy(W, dir_, waves=8):
+    """Restatement of pack_quad_kernel (pntf_quad.h): the wave streams of one layer,
+    shape (wave, groups, IN/16, 64 lanes, 4); block (og, kb) rows rotated by kb."""
     A = W.T if dir_ else W
     OUT, IN = A.shape
-    w, g, q, lane, e = np.meshgrid(np.arange(4), np.arange(OUT // 64), np.arange(IN // 16),
-                                   np.arange(64), np.arange(4), indexing="ij")
-    row = w * (OUT // 4) + 16 * g + 4 * (lane >> 4) + (lane & 3)
-    k = 16 * q + 4 * e + ((lane >> 2) & 3)
+    w, g, q, lane, e = np.meshgrid(np.arange(waves), np.arange(OUT // (16 * waves)),
+                                   np.arange(IN // 16), np.arange(64), np.arange(4),
+                                   indexing="ij")
+    kb = (lane >> 2) & 3
+    row = w * (OUT // waves) + 16 * g + 4 * (lane >> 4) + ((lane + kb) & 3)
+    k = 16 * q + 4 * e + kb
     return A[row, k]
+
+
+def _ror16(x, n):
+    """DPP row_ror:n: lane i of each 16-lane row reads lane (i - n) mod 16."""
+    lane = np.arange(64)
+    return x[(lane & ~15) | ((lane - n) & 15)]
 
 
 def test_quad_pack_feeds_4x4x1_blocks():
     """Emulate one quad layer on the packed stream: v_mfma_f32_4x4x1_16b_f32 gives lane l
     D[i] += A(lane 4 (l >> 2) + i) * B(lane l) (block l >> 2, row i, column l & 3; layout
-    measured by tests/diag/quad_probe.hip), B lane l = act[4 s + kb][pair l & 3]; after the
-    sum over the k sub-blocks kb (lanes l ^ 4, l ^ 8) lane (og, kb, j) keeps D[kb] = the
-    layer output at row w·OUT/4 + 16 g + 4 og + kb, pair j."""
+    measured by tests/diag/quad_probe.hip), B lane l = act[4 s + kb][pair l & 3]; the DPP tree
+    of qring_sum leaves lane (og, kb, j) with the layer output at row
+    w·OUT/8 + 16 g + 4 og + kb, pair j.  The SOLO layer (VALU, one pair; qring_sum_solo) reads
+    the same partials from its lanes and sums them in the same association: bit-identical."""
     rng = np.random.default_rng(2)
     for (rows, cols, dir_) in [(128, 256, 0), (256, 128, 1), (256, 256, 0)]:
-        W = rng.standard_normal((rows, cols)).astype(np.float64)
+        W = rng.standard_normal((rows, cols)).astype(np.float32)
         P = _pack_quad_numpy(W, dir_)
         A = W.T if dir_ else W
         OUT, IN = A.shape
-        act = rng.standard_normal((IN, 4))
-        ref = A @ act
+        act = rng.standard_normal((IN, 4)).astype(np.float32)
+        ref = A.astype(np.float64) @ act.astype(np.float64)
         lane = np.arange(64)
         og, kb, j = lane >> 4, (lane >> 2) & 3, lane & 3
-        for w in range(4):
-            for g in range(OUT // 64):
-                D = np.zeros((64, 4))
+        for w in range(8):
+            for g in range(OUT // 128):
+                D = np.zeros((64, 4), np.float32)
                 for q in range(IN // 16):
                     for e in range(4):
                         s = 4 * q + e
@@ -209,11 +218,25 @@ def test_quad_pack_feeds_4x4x1_blocks():
                         b = act[4 * s + kb, j]
                         for i in range(4):
                             D[:, i] += a[4 * (lane >> 2) + i] * b
-                S = D + D[lane ^ 4]
-                S = S + S[lane ^ 8]
-                v = S[lane, kb]
-                rws = w * (OUT // 4) + 16 * g + 4 * og + kb
-                np.testing.assert_allclose(v, ref[rws, j], rtol=1e-12, atol=1e-9)
+                b = D[:, 0] + _ror16(D[:, 1], 4)
+                a = D[:, 2] + _ror16(D[:, 3], 4)
+                p = b + _ror16(a, 8)
+                rws = w * (OUT // 8) + 16 * g + 4 * og + kb
+                np.testing.assert_allclose(p, ref[rws, j], rtol=1e-4, atol=1e-3)
+                # the unrotated layout's butterflies (rounds 1-4) sum the same partials in the
+                # same association: identical bits
+                S = np.zeros((64, 4), np.float32)
+                for i in range(4):
+                    S[lane, (i + kb) & 3] = D[:, i]
+                S = S + S[(lane & ~15) | ((lane - 4) & 15)]
+                S = S + S[(lane & ~15) | ((lane - 8) & 15)]
+                assert np.array_equal(p, S[lane, kb])
+                # SOLO for pair 0: lane (og, kb, r) holds its own-row partial, = D[4 (l >> 2)
+                # + 0][r] of the MFMA path (row (r + kb) & 3, pair 0)
+                t = D[4 * (lane >> 2), lane & 3]
+                bs = t + _ror16(t, 3)
+                solo = (bs + _ror16(bs, 6))[lane & ~3]
+                assert np.array_equal(solo, p[lane & ~3])
 
 
 def test_synth_is_deterministic():

@@ -146,10 +146,35 @@ __device__ __forceinline__ float pair_sum(float v) {
   return v;
 }
 
+// Bias vectors per layer: one value per group of 16 out rows the wave owns (qg(256) of them at
+// most: 2 with 8 waves), so 14 of them take 28 VGPRs, not the 56 of a 4-group vector.  The
+// head bias generator.4.bias rides in aux[13][qg(128)], a slot generator[-2] does not use.
+constexpr int QAUXW = 256 / (16 * Q_WAVES);
+static_assert(QAUXW == 2 || QAUXW == 4, "quad bias vector width");
+typedef float qaux_t __attribute__((ext_vector_type(QAUXW)));
+constexpr int QAUX_G4B = 128 / (16 * Q_WAVES);
+// pack_quad_aux_kernel stores 4 groups per lane (16 bytes); the first QAUXW are the used ones
+__device__ __forceinline__ qaux_t qaux_load(Rsrc AX, int lane, int i) {
+  qaux_t r;
+  if constexpr (QAUXW == 4) {
+    const f32x4 t = bload(AX, lane * 16, i * 1024);
+#pragma unroll
+    for (int k = 0; k < QAUXW; ++k) r[k] = t[k % 4];
+  } else {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 t = __builtin_bit_cast(
+        f32x2, __builtin_amdgcn_raw_buffer_load_b64(AX, lane * 16, i * 1024, 0));
+#pragma unroll
+    for (int k = 0; k < QAUXW; ++k) r[k] = t[k % 2];
+  }
+  return r;
+}
 // v[g] for a runtime group index (explicit selects: a dynamic vector index would put the
 // vector on the stack)
-__device__ __forceinline__ float pick(const f32x4& v, int g) {
-  return g == 0 ? v[0] : g == 1 ? v[1] : g == 2 ? v[2] : v[3];
+template <int N = QAUXW>
+__device__ __forceinline__ float pick(const qaux_t& v, int g) {
+  if constexpr (N == 2) return g == 0 ? v[0] : v[1];
+  else return g == 0 ? v[0] : g == 1 ? v[1] : g == 2 ? v[2] : v[3];
 }
 
 struct QCx {
@@ -321,7 +346,7 @@ __device__ __forceinline__ void qreduce(const QCx& cx, float (&v)[NV]) {
 // GRAD: save σ10 for the reverse sweep.  Buffers: 0 = features / dz, 1 = A, 2 = B.
 template <int DIM, bool GRAD, int NF, int QR, bool SOLO = false>
 __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx& cx,
-                                              const PairIO& io, const f32x4 (&aux)[Q_NAUX],
+                                              const PairIO& io, const qaux_t (&aux)[Q_NAUX],
                                               int compat) {
   const float cm = compat ? 1.f : 0.f;
   lds_f *F = cx.buf(0), *A = cx.buf(1), *B = cx.buf(2);
@@ -402,8 +427,8 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
   // body is a macro: as a lambda called with a runtime block index it put `aux` on the stack.)
 #define PNTF_QGEN_FWD(i, S0A, S0B, WA, WB)                                                                 \
   {                                                                                                \
-    const f32x4 ba = (i) == 0 ? aux[6] : (i) == 1 ? aux[8] : aux[10];                              \
-    const f32x4 bb = (i) == 0 ? aux[7] : (i) == 1 ? aux[9] : aux[11];                              \
+    const qaux_t ba = (i) == 0 ? aux[6] : (i) == 1 ? aux[8] : aux[10];                              \
+    const qaux_t bb = (i) == 0 ? aux[7] : (i) == 1 ? aux[9] : aux[11];                              \
     qlayer<1, 256, NF, qg(256), S0A, QR, SOLO, WA>(ring, W, cx, B, [&](int g, const float (&v)[1]) {   \
       SpSig q = sp_sig(v[0] + pick(ba, g));                                                        \
       *cx.at<256>(A, 0, g) = q.sp;                                                                 \
@@ -438,7 +463,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
     if (GRAD) *cx.sig(QS_G3 + g) = q.sg;
   });
   qreduce<1>(cx, part);
-  const float y4 = part[0] + aux[13][2];
+  const float y4 = part[0] + aux[13][QAUX_G4B];
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-0.144269504088896341f * y4));
 }
 
@@ -447,7 +472,7 @@ __device__ __forceinline__ float quad_forward(QRing<QR>& ring, Rsrc W, const QCx
 template <int DIM, int NF, int QR, bool SOLO = false>
 __device__ __forceinline__ void quad_backward(QRing<QR>& ring, Rsrc W, const QCx& cx,
                                               const PairIO& io, float tau,
-                                              const f32x4 (&aux)[Q_NAUX], float (&ds)[DIM],
+                                              const qaux_t (&aux)[Q_NAUX], float (&ds)[DIM],
                                               float (&dg)[DIM]) {
   lds_f *F = cx.buf(0), *A = cx.buf(1), *B = cx.buf(2);
   // ---- head and generator[-2] (:592-613): dv = d · G4 ⊙ σ10(y3) -> A (128 rows)
@@ -578,6 +603,9 @@ __device__ __forceinline__ QCx quad_cx(lds_f* lds) {
   cx.kb = (cx.lane >> 2) & 3;
   cx.l16 = cx.lane & 15;
   cx.sp = 0;
+#if defined(PNTF_QPRIO) && PNTF_QPRIO   // diagnostics: static priority for the second wave half
+  if (cx.w >= Q_WAVES / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   return cx;
 }
 
@@ -592,10 +620,10 @@ __global__ __launch_bounds__(64 * Q_WAVES, 1) void field_quad_kernel(FieldArgs a
   const QCx cx = quad_cx((lds_f*)smem);
   const Rsrc W = make_rsrc(a.P + OFF_QUAD + cx.w * Q_STREAM, Q_STREAM * 4);
   const Rsrc AX = make_rsrc(a.P + OFF_QUAD + Q_OFF_AUX + cx.w * Q_NAUX * 256, Q_NAUX * 1024);
-  f32x4 aux[Q_NAUX];
+  qaux_t aux[Q_NAUX];
 #pragma unroll
-  for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
-  aux[13][2] = a.P[OFF_BIAS + B_G4B];
+  for (int i = 0; i < Q_NAUX; ++i) aux[i] = qaux_load(AX, cx.lane, i);
+  aux[13][QAUX_G4B] = a.P[OFF_BIAS + B_G4B];
   QRing<QR> ring;
   ring.off = 0;
 #pragma unroll
@@ -648,10 +676,10 @@ __global__ __launch_bounds__(64 * Q_WAVES, 1) void plan_quad_kernel(PlanArgs a) 
   int32_t* const tail_it = tail ? tail + 2 + a.q : nullptr;
   const Rsrc W = make_rsrc(a.P + OFF_QUAD + cx.w * Q_STREAM, Q_STREAM * 4);
   const Rsrc AX = make_rsrc(a.P + OFF_QUAD + Q_OFF_AUX + cx.w * Q_NAUX * 256, Q_NAUX * 1024);
-  f32x4 aux[Q_NAUX];
+  qaux_t aux[Q_NAUX];
 #pragma unroll
-  for (int i = 0; i < Q_NAUX; ++i) aux[i] = bload(AX, cx.lane * 16, i * 1024);
-  aux[13][2] = a.P[OFF_BIAS + B_G4B];
+  for (int i = 0; i < Q_NAUX; ++i) aux[i] = qaux_load(AX, cx.lane, i);
+  aux[13][QAUX_G4B] = a.P[OFF_BIAS + B_G4B];
   constexpr int QR = SOLO ? QRING_SOLO : QRING;
   QRing<QR> ring;
   ring.off = 0;

@@ -110,8 +110,10 @@ __device__ __forceinline__ f32x16 wload(WScratch sc, int t, int lane) {
 // 1 KiB contiguous (lane-major f32x4), so ds_write_b128 / ds_read_b128 are conflict-free.
 typedef __attribute__((address_space(3))) f32x4 wlds_f4;
 constexpr int WL_G3 = 0, WL_S0 = 4, WL_TILES = 8;
+typedef __attribute__((address_space(3))) float wlds_f;
 struct WLds {
-  wlds_f4* p;   // this wave's region, offset by the lane
+  wlds_f4* p;          // this wave's region, offset by the lane
+  const wlds_f* hw;    // the head row generator.4.weight (128 floats, staged once per workgroup)
 };
 __device__ __forceinline__ void lstore(WLds l, int t, const f32x16& v) {
 #pragma unroll
@@ -295,13 +297,17 @@ __device__ __forceinline__ f32x4 wbw_load(const float* p) {
   return ld4(p);
 #endif
 }
-__device__ __forceinline__ f32x4 whw_load(Rsrc W, int lane, int off) {
+// head-row features 32 t + 8 u + 4 h .. + 3 (the rows of registers 4u..4u+3 of tile t): an
+// LDS broadcast read (half the lanes share each address).  From the packed blob these 16
+// loads per pass were sunk to their use and each waited out an L2 round trip with the whole
+// weight ring (vmcnt(0)); tests/diag ablation: -0.5 % kernel time.
+__device__ __forceinline__ f32x4 whw_load(const WLds& wl, int t, int u, int h) {
 #ifdef PNTF_ABL_NOHW
-  float v = 1e-3f * (float)((lane + off) & 255);
+  float v = 1e-3f * (float)((t * 4 + u + h) & 255);
   asm volatile("v_mov_b32 %0, %0" : "+v"(v));
   return f32x4{v, v + 1e-4f, v + 2e-4f, v + 3e-4f};
 #else
-  return bload(W, lane * 16, off);
+  return *reinterpret_cast<const wlds_f4*>(wl.hw + 32 * t + 8 * u + 4 * h);
 #endif
 }
 
@@ -468,7 +474,7 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 w = whw_load(W, lane, WHW + ((4 * t + u) * 64) * 16);
+      f32x4 w = whw_load(wl, t, u, h);
 #pragma unroll
       for (int s = 0; s < 4; ++s) part = fmaf(w[s], Y[t][4 * u + s], part);
     }
@@ -494,7 +500,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
     f32x16 s3 = lload(wl, WL_G3 + t);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 w = whw_load(W, lane, WHW + ((4 * t + u) * 64) * 16);
+      f32x4 w = whw_load(wl, t, u, h);
 #pragma unroll
       for (int s = 0; s < 4; ++s) Y[t][4 * u + s] = (dd * w[s]) * s3[4 * u + s];
     }
@@ -623,9 +629,14 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
       make_wscratch(GRAD ? a.ws + (int64_t)slot * WSCRATCH_FLOATS_PER_WAVE : nullptr);
   const Rsrc W = make_rsrc(a.P, PACKED_TOTAL * 4);
   __shared__ f32x4 wsig[GRAD ? WAVES * WL_TILES * 4 * 64 : 1];
-  const WLds wl{(wlds_f4*)wsig +
-                (GRAD ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (WL_TILES * 4 * 64) + lane
-                      : 0)};
+  // each wave keeps its own copy of the head row (no workgroup barrier: a wave's LDS reads
+  // follow its own writes in order)
+  __shared__ f32x4 whead[WAVES * H / 4];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const WLds wl{(wlds_f4*)wsig + (GRAD ? wv * (WL_TILES * 4 * 64) + lane : 0),
+                (const wlds_f*)(whead + wv * (H / 4))};
+  ((wlds_f*)(whead + wv * (H / 4)))[lane] = a.P[OFF_BIAS + B_G4W + lane];
+  ((wlds_f*)(whead + wv * (H / 4)))[lane + 64] = a.P[OFF_BIAS + B_G4W + lane + 64];
   Ring ring;
   ring_fill<4>(ring, W, lane * 16, WE0Head{});
   for (int tile = slot; tile < ntiles; tile += nslots) {

@@ -15,7 +15,7 @@ template <int DIM, int KIND>
 __global__ void field_kernel(FieldArgs a);
 template <int DIM, int KIND>
 __global__ void field_split_kernel(FieldArgs a);
-template <int DIM, int KIND>
+template <int DIM, int KIND, bool BL>
 __global__ void wide_field_kernel(FieldArgs a);
 template <int DIM>
 __global__ void plan_kernel(PlanArgs a);
@@ -186,22 +186,29 @@ static void launch_quad(int kind, int64_t grid, const FieldArgs& a, hipStream_t 
   }
 }
 
+template <int DIM, bool BL>
+static void launch_wide(int kind, dim3 g, dim3 b, const FieldArgs& a, hipStream_t s) {
+  switch (kind) {
+    case K_TAU: hipLaunchKernelGGL((wide_field_kernel<DIM, K_TAU, BL>), g, b, 0, s, a); break;
+    case K_TAU_GRAD:
+      hipLaunchKernelGGL((wide_field_kernel<DIM, K_TAU_GRAD, BL>), g, b, 0, s, a);
+      break;
+    case K_VELOCITY:
+      hipLaunchKernelGGL((wide_field_kernel<DIM, K_VELOCITY, BL>), g, b, 0, s, a);
+      break;
+    case K_SPEED: hipLaunchKernelGGL((wide_field_kernel<DIM, K_SPEED, BL>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((wide_field_kernel<DIM, K_TRAVEL, BL>), g, b, 0, s, a); break;
+  }
+}
+
 template <int DIM>
 static void launch_field(int kind, int64_t grid, const FieldArgs& a, hipStream_t s,
                          bool split, bool wide) {
   dim3 g((unsigned)grid), b(split ? 64 * SPLIT_WAVES : 256);
   if (wide) {
-    switch (kind) {
-      case K_TAU: hipLaunchKernelGGL((wide_field_kernel<DIM, K_TAU>), g, b, 0, s, a); break;
-      case K_TAU_GRAD:
-        hipLaunchKernelGGL((wide_field_kernel<DIM, K_TAU_GRAD>), g, b, 0, s, a);
-        break;
-      case K_VELOCITY:
-        hipLaunchKernelGGL((wide_field_kernel<DIM, K_VELOCITY>), g, b, 0, s, a);
-        break;
-      case K_SPEED: hipLaunchKernelGGL((wide_field_kernel<DIM, K_SPEED>), g, b, 0, s, a); break;
-      default: hipLaunchKernelGGL((wide_field_kernel<DIM, K_TRAVEL>), g, b, 0, s, a); break;
-    }
+    // the env-B table in LDS when it fits (identical values, so identical results)
+    if ((int64_t)a.n_env * DIM * H <= WBL_FLOATS) launch_wide<DIM, true>(kind, g, b, a, s);
+    else launch_wide<DIM, false>(kind, g, b, a, s);
     return;
   }
   if (split) {

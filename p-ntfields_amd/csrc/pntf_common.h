@@ -89,6 +89,9 @@ static_assert(Q_WAVES == 4 || Q_WAVES == 8, "quad layers: 4 or 8 waves per workg
 constexpr int Q_NL = 26;
 constexpr int Q_STREAM = 2 * SZ_DIR / Q_WAVES;      // floats of one wave's fragment stream
 constexpr int Q_NF_FWD = SZ_DIR / Q_WAVES / 256;    // 1 KiB fragments of its forward part
+// env-B table staged in LDS by the wide kernels when n_env · dim · 128 floats fit (pntf_wide.h
+// WBt<true>): 20 KiB, i.e. dim 3 up to 13 environments, dim 6 up to 6
+constexpr int WBL_FLOATS = 5120;
 constexpr int Q_NAUX = 14;
 constexpr int OFF_QUAD = (OFF_WIDE + W_SZ + 63) / 64 * 64;
 constexpr int Q_OFF_AUX = Q_WAVES * Q_STREAM;

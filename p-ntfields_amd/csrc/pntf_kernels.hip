@@ -19,7 +19,8 @@ template __global__ void field_quad_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
 #elif defined(PNTF_PLAN_QUAD)
 template __global__ void plan_quad_kernel<PNTF_DIM, PNTF_QSOLO>(PlanArgs);
 #elif defined(PNTF_KIND) && defined(PNTF_WIDE_FIELD)
-template __global__ void wide_field_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
+template __global__ void wide_field_kernel<PNTF_DIM, PNTF_KIND, false>(FieldArgs);
+template __global__ void wide_field_kernel<PNTF_DIM, PNTF_KIND, true>(FieldArgs);
 #elif defined(PNTF_KIND) && defined(PNTF_SPLIT_FIELD)
 template __global__ void field_split_kernel<PNTF_DIM, PNTF_KIND>(FieldArgs);
 #elif defined(PNTF_KIND)

@@ -297,6 +297,27 @@ __device__ __forceinline__ f32x4 wbw_load(const float* p) {
   return ld4(p);
 #endif
 }
+// Where a lane reads its environment's B rows: global memory (any table), or the table staged
+// in LDS once per workgroup when it fits (WBL_FLOATS; pntf_capi.hip picks the kernel).  The LDS
+// reads take the Fourier projections' and the fold's B loads off the in-order vmcnt queue.
+template <bool BL>
+struct WBt {
+  __device__ __forceinline__ f32x4 load(const PairIO& io, int i) const {
+    return wbw_load(io.Bw + i);
+  }
+};
+template <>
+struct WBt<true> {
+  const wlds_f* t;   // this lane's environment in the staged table
+  __device__ __forceinline__ f32x4 load(const PairIO&, int i) const {
+#ifdef PNTF_ABL_NOBW
+    return wbw_load(reinterpret_cast<const float*>(static_cast<uintptr_t>(i)));
+#else
+    return *reinterpret_cast<const wlds_f4*>(t + i);
+#endif
+  }
+};
+
 // head-row features 32 t + 8 u + 4 h .. + 3 (the rows of registers 4u..4u+3 of tile t): an
 // LDS broadcast read (half the lanes share each address).  From the packed blob these 16
 // loads per pass were sunk to their use and each waited out an L2 round trip with the whole
@@ -314,15 +335,16 @@ __device__ __forceinline__ f32x4 whw_load(const WLds& wl, int t, int u, int h) {
 // ---------------------------------------------------------------- Fourier projections
 // q[c][r] = x_c · 2πB[:, 32 kt + row(r, h)] for the lane's 16 feature rows of Fourier tile
 // kt, both points; the B rows come from the pair's environment (io.Bw, dim x 128).
-template <int DIM>
-__device__ __forceinline__ void wfourier_q(const PairIO& io, int kt, int h, f32x16 (&q)[2]) {
+template <int DIM, class BT>
+__device__ __forceinline__ void wfourier_q(const PairIO& io, const BT& bt, int kt, int h,
+                                           f32x16 (&q)[2]) {
 #pragma unroll
   for (int c = 0; c < 2; ++c) q[c] = zero16();
 #pragma unroll
   for (int d = 0; d < DIM; ++d)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 b = wbw_load(io.Bw + d * H + 32 * kt + 8 * u + 4 * h);
+      f32x4 b = bt.load(io, d * H + 32 * kt + 8 * u + 4 * h);
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -333,8 +355,8 @@ __device__ __forceinline__ void wfourier_q(const PairIO& io, int kt, int h, f32x
 // ---------------------------------------------------------------- forward pass
 // NN.out on 32 pairs.  GRAD: save σ tiles.  On entry the ring holds WE0Head; on return the
 // first PF steps of `after`.  Returns τ of the lane's pair (same in both lane halves).
-template <int DIM, bool GRAD, class AfterF>
-__device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& io,
+template <int DIM, bool GRAD, class BT, class AfterF>
+__device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& io, BT bt,
                                               f32x16 (&X)[8], f32x16 (&Y)[8], WScratch sc,
                                               WLds wl, int compat, int lane, AfterF after) {
   const int h = lane >> 5;
@@ -348,7 +370,7 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
   be0.load(W, lane, B_E0);
   {
     f32x16 q[2], sn[2];
-    wfourier_q<DIM>(io, 0, h, q);
+    wfourier_q<DIM>(io, bt, 0, h, q);
     run_steps<32, 4, 4, SITE_FWD_E0>(
         ring, W, lane * 16, WE0Head{}, WHead{WF + OFF_EBLK * 4},
         [&](auto st, const f32x4 (&a)[4]) {
@@ -381,7 +403,7 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
                 X[c * 4 + ot] = mfma32(a[u][s], b, X[c * 4 + ot]);
               }
           // next sin/cos tile's projections, after this tile's MFMAs are issued
-          if constexpr (ot == 3 && kt < 3) wfourier_q<DIM>(io, kt + 1, h, q);
+          if constexpr (ot == 3 && kt < 3) wfourier_q<DIM>(io, bt, kt + 1, h, q);
           if constexpr (S == 16) a0bc.load(W, lane, B_EBLK);
         });
   }
@@ -487,9 +509,10 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
 // Exact reverse mode (or out_backgrad when the forward stored the quirk).  On entry the ring
 // holds wbwd_head(); on return the first PF steps of `after`.  ds/dg: dτ/dxs, dτ/dxg of the
 // lane's pair (same in both halves).
-template <int DIM, class AfterF>
-__device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& io, float tau,
-                                              f32x16 (&X)[8], f32x16 (&Y)[8], WScratch sc,
+template <int DIM, class BT, class AfterF>
+__device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& io, BT bt,
+                                              float tau, f32x16 (&X)[8], f32x16 (&Y)[8],
+                                              WScratch sc,
                                               WLds wl, int lane, float (&ds)[DIM],
                                               float (&dg)[DIM], AfterF after) {
   const int h = lane >> 5;
@@ -589,7 +612,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
           for (int u = 0; u < 4; ++u) {
             f32x4 bw[DIM];
 #pragma unroll
-            for (int d = 0; d < DIM; ++d) bw[d] = TWO_PI * wbw_load(io.Bw + d * H + 32 * o + 8 * u + 4 * h);
+            for (int d = 0; d < DIM; ++d) bw[d] = TWO_PI * bt.load(io, d * H + 32 * o + 8 * u + 4 * h);
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -615,7 +638,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
 }
 
 // ---------------------------------------------------------------- kernel
-template <int DIM, int KIND>
+template <int DIM, int KIND, bool BL>
 __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
   constexpr bool GRAD = KIND != K_TAU && KIND != K_TRAVEL;
   const int lane = threadIdx.x & 63;
@@ -637,8 +660,15 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
                 (const wlds_f*)(whead + wv * (H / 4))};
   ((wlds_f*)(whead + wv * (H / 4)))[lane] = a.P[OFF_BIAS + B_G4W + lane];
   ((wlds_f*)(whead + wv * (H / 4)))[lane + 64] = a.P[OFF_BIAS + B_G4W + lane + 64];
+  __shared__ f32x4 wbtab[BL ? WBL_FLOATS / 4 : 1];
+  if constexpr (BL) {   // the host checked n_env · DIM · H <= WBL_FLOATS
+    const int nb4 = a.n_env * (DIM * H / 4);
+    for (int i = threadIdx.x; i < nb4; i += 256)
+      wbtab[i] = *reinterpret_cast<const f32x4*>(a.Btab + 4 * i);
+  }
   Ring ring;
   ring_fill<4>(ring, W, lane * 16, WE0Head{});
+  if constexpr (BL) __syncthreads();
   for (int tile = slot; tile < ntiles; tile += nslots) {
     f32x16 X[8], Y[8];
     // the pair column, re-derived per tile from the lane·16 byte offset every load keeps
@@ -649,15 +679,17 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
     const int64_t pair = (int64_t)(tile * WTILE + ((v16 >> 4) & 31));
     PairIO io;
     const bool ok = load_pair<DIM>(a.xp, a.Btab, a.env, a.n, a.n_env, pair, io);
+    WBt<BL> bt;
+    if constexpr (BL) bt.t = (const wlds_f*)wbtab + (io.Bw - a.Btab);
     float tau;
     if constexpr (GRAD)
-      tau = wide_forward<DIM, true>(ring, W, io, X, Y, sc, wl, a.compat, lane, wbwd_head());
+      tau = wide_forward<DIM, true>(ring, W, io, bt, X, Y, sc, wl, a.compat, lane, wbwd_head());
     else
-      tau = wide_forward<DIM, false>(ring, W, io, X, Y, sc, wl, a.compat, lane, WE0Head{});
+      tau = wide_forward<DIM, false>(ring, W, io, bt, X, Y, sc, wl, a.compat, lane, WE0Head{});
     float ds[DIM], dg[DIM];
     if constexpr (GRAD) {
       drain_stores();
-      wide_backward<DIM>(ring, W, io, tau, X, Y, sc, wl, lane, ds, dg, WE0Head{});
+      wide_backward<DIM>(ring, W, io, bt, tau, X, Y, sc, wl, lane, ds, dg, WE0Head{});
     }
     const bool store = lane < 32 && pair < a.n;
     store_field<DIM, KIND>(a, pair, ok, store, tau, io, ds, dg);

@@ -27,7 +27,11 @@ extern "C" int perf_tau_grad(int grid, const float* P, const float* xp, int64_t 
   using namespace pntf;
   FieldArgs a{P, xp, Btab, nullptr, n, 1, 0, tau, dtau, ws};
 #ifdef PERF_WIDE
-  hipLaunchKernelGGL((wide_field_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(256), 0, stream, a);
+#ifndef PERF_WBL
+#define PERF_WBL 0
+#endif
+  hipLaunchKernelGGL((wide_field_kernel<3, K_TAU_GRAD, PERF_WBL>), dim3(grid), dim3(256), 0,
+                     stream, a);
 #elif defined(PERF_QUAD)    // one workgroup per 4-pair tile
   hipLaunchKernelGGL((field_quad_kernel<3, K_TAU_GRAD>), dim3(grid), dim3(64 * Q_WAVES), 0,
                      stream, a);

@@ -145,6 +145,23 @@ def test_invalid_env_gives_nan(packed, dev, field_schedule):
     assert np.isfinite(t[ok]).all() and np.isfinite(d[ok]).all()
 
 
+@pytest.mark.parametrize("dim,fit", [(3, 13), (6, 6)])
+def test_wide_env_table_in_lds_matches_global(packed, dev, dim, fit):
+    """The wide kernels stage the env-B table in LDS when n_env · dim · 128 floats fit in
+    WBL_FLOATS (pntf_common.h; 13 envs at dim 3, 6 at dim 6) and read it from global memory
+    otherwise.  Same pairs and env ids, the table padded by one more environment so that it no
+    longer fits: bitwise equal results, at the limit and one below it."""
+    n = 2 * 32 * 257
+    xp = T(synth.make_pairs(n, dim, seed=41), dev)
+    for E in (fit, fit - 1):
+        Bt = synth.make_B_table(E + 1, dim, first_seed=60)
+        env = T(synth.make_env_ids(n, E, contiguous=False, seed=E), dev, torch.int32)
+        t_l, d_l = ops.tau_grad(packed, xp, T(Bt[:E], dev), env, dim=dim, schedule="wide_tile")
+        t_g, d_g = ops.tau_grad(packed, xp, T(Bt, dev), env, dim=dim, schedule="wide_tile")
+        assert torch.equal(t_l, t_g) and torch.equal(d_l, d_g)
+        assert torch.isfinite(t_l).all()
+
+
 def test_coincident_endpoints(packed, dev, W):
     """xs == xg: τ and ∇τ are finite (the merge is symmetric), Speed = τ."""
     x = synth.make_pairs(8, 3, seed=9)

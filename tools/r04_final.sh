@@ -1,4 +1,4 @@
-# Round-4 final pass on one GPU (24-deep quad ring, NN.out weight tape, C2 warm-up): the -m gpu suite, the C5
+# Round-4 final pass on one GPU (pinned 16-deep quad ring, wide head row + env-B table in LDS): the -m gpu suite, the C5
 # planner (stats + PMC passes), the stream probes, the Q1 planner step, the headline profile
 # (tools/profile_round.sh: stats + FETCH/WRITE/MFMA/stall PMC), then the default bench line.
 # Outputs in gpurun_out/; tools/prof_summary.py and tools/c5_pmc_summary.py turn them into

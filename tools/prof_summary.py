@@ -34,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--pairs", type=int, default=1 << 20)
-    ap.add_argument("--kernel", default="wide_field_kernel<3, 1>")
+    ap.add_argument("--kernel", default="wide_field_kernel<3, 1, true>")
     ap.add_argument("--unit", default="wide_d3_k1", help="build unit of --kernel")
     a = ap.parse_args()
     import sys

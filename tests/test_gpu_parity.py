@@ -450,6 +450,30 @@ def test_headline_1m_sample_vs_fp64_oracle(packed, dev, W):
     assert e_hip <= max(1e-4, 1.5 * e_ref)
 
 
+def test_c4_shape_sharded_on_one_gpu(packed, dev, W):
+    """BASELINE C4 at its full size on one GPU: 8 x 1 048 576 (+ 5, so the shards are uneven)
+    Gibson pairs, 10 envs, per-pair env id.  Each of the 8 rank shards (pntf.dist.shard_range,
+    the bench's N > 1 split) evaluated alone equals the same rows of the whole batch bit for
+    bit, so the sharded job's all-gathered output is the single-batch output; a 256-pair sample
+    of the whole batch against the fp64 oracle."""
+    from pntf import dist
+    n, ws = 8 * (1 << 20) + 5, 8
+    xp_np = synth.make_pairs(n, 3, seed=2024)
+    Bt_np = synth.make_B_table(10, 3)
+    env_np = synth.make_env_ids(n, 10)
+    xp, Bt, env = T(xp_np, dev), T(Bt_np, dev), T(env_np, dev, torch.int32)
+    t, d = ops.tau_grad(packed, xp, Bt, env, dim=3)
+    assert torch.isfinite(t).all() and torch.isfinite(d).all()
+    for r in range(ws):
+        lo, hi = dist.shard_range(n, r, ws)
+        ts, dsh = ops.tau_grad(packed, xp[lo:hi].contiguous(), Bt, env[lo:hi].contiguous(), dim=3)
+        assert torch.equal(ts, t[lo:hi]) and torch.equal(dsh, d[lo:hi]), r
+    idx = np.random.default_rng(8).choice(n, 256, replace=False)
+    to, do = O.tau_grad(W, xp_np[idx], Bt_np, env_np[idx])
+    close(t.cpu().numpy()[idx], to[:, 0])
+    close(d.cpu().numpy()[idx], do)
+
+
 def test_device_sum_deterministic(dev):
     x = torch.from_numpy(np.random.default_rng(0).standard_normal(1000003).astype(np.float32)).to(dev)
     a, b = ops.device_sum(x), ops.device_sum(x)

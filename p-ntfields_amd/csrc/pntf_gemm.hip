@@ -321,6 +321,9 @@ struct PanelArgs {
   const f32x4* P;
   float* C;
   int64_t M, lda, ldc;
+  const float* Cin;   // ACC: the added matrix (C itself, or another one of C's layout)
+  const float* bias;  // LDS kernel, ACC: bias[col] added to rows < brows first (else null)
+  int64_t brows;
 };
 
 __global__ void panel_pack_kernel(const float* __restrict__ W, int64_t ldb, int tb, int KC,
@@ -385,7 +388,7 @@ __global__ __launch_bounds__(256, PNTF_PANEL_WPS) void panel_gemm_kernel(PanelAr
     const int64_t next = tile + stride;
     const bool more = next < ntiles;
     const Rsrc rn = win(g.A, g.lda, more ? next : tile);
-    const Rsrc rc = win(g.C, g.ldc, tile);
+    const Rsrc rc = win(g.C, g.ldc, tile), rci = win(g.Cin, g.ldc, tile);
     f32x16 acc[4];
     f32x4 cb[4][4];
     pg_static_for<0, NQ>([&](auto I) {
@@ -400,7 +403,7 @@ __global__ __launch_bounds__(256, PNTF_PANEL_WPS) void panel_gemm_kernel(PanelAr
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int R = 0; R < 4; ++R) cb[t][R] = pg_load(rc, vc, (32 * (4 * G + t) + 8 * R) * 4);
+          for (int R = 0; R < 4; ++R) cb[t][R] = pg_load(rci, vc, (32 * (4 * G + t) + 8 * R) * 4);
       }
       // prefetch PF iterations ahead; past the tile's end the stream wraps to the next tile
       constexpr int pit = (it + PF) % NQ;
@@ -465,10 +468,13 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
     wg = (s >> 1) * 8 + x;
     nwg = gridDim.x / 2;
   }
+  __shared__ f32x4 lb[ACC ? 32 : 1];   // the group's 128 bias columns (ACC with a bias)
   {   // stage the group's fragments (contiguous in P: out tiles 4·grp .. 4·grp + 3)
     const f32x4* src = g.P + (int64_t)grp * FR * 64;
 #pragma unroll 8
     for (int i = threadIdx.x; i < FR * 64; i += 256) lw[i] = src[i];
+    if (ACC && g.bias && threadIdx.x < 32)
+      lb[threadIdx.x] = *reinterpret_cast<const f32x4*>(g.bias + 128 * grp + 4 * threadIdx.x);
   }
   __syncthreads();
   const int64_t ntiles = (g.M + 31) / 32;
@@ -495,7 +501,7 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
     const int64_t next = tile + stride;
     const bool more = next < ntiles;
     const Rsrc rn = win(g.A, g.lda, more ? next : tile);
-    const Rsrc rc = win(g.C, g.ldc, tile);
+    const Rsrc rc = win(g.C, g.ldc, tile), rci = win(g.Cin, g.ldc, tile);
     f32x16 acc[4];
     f32x4 cb[4][4];
 #pragma unroll
@@ -508,7 +514,7 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int R = 0; R < 4; ++R) cb[t][R] = pg_load(rc, vc, (c0 + 32 * t + 8 * R) * 4);
+          for (int R = 0; R < 4; ++R) cb[t][R] = pg_load(rci, vc, (c0 + 32 * t + 8 * R) * 4);
       }
       // next iteration's fragments (past the tile's end: the next tile's first ones)
       constexpr int qn = (q + 1) % QK;
@@ -523,12 +529,17 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
       }
       if (more) x[q] = pg_load(rn, va, 32 * q);   // x[q] is dead for this tile: next panel
       if constexpr (q == QK - 1) {
+        // (acc + bias) + C: the order of nn.Linear's addmm and the residual add after it
+        const bool brow = ACC && g.bias && 32 * tile + j < g.brows;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int R = 0; R < 4; ++R) {
             f32x4 v = {acc[t][4 * R], acc[t][4 * R + 1], acc[t][4 * R + 2], acc[t][4 * R + 3]};
-            if (ACC) v += cb[t][R];
+            if (ACC) {
+              if (brow) v += lb[8 * t + 2 * R + h];
+              v += cb[t][R];
+            }
             pg_store(rc, v, vc, (c0 + 32 * t + 8 * R) * 4);
           }
       }
@@ -1279,9 +1290,34 @@ size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K) {
   return big > wgrad ? big : wgrad;
 }
 
+// The panel GEMMs' conditions (C = A·op(B) (+ Cin) on the register-panel / LDS-panel kernels)
+static bool panel_path(int ta, int64_t N, int64_t K, int64_t lda, int64_t ldc, float beta,
+                       const float* A, const float* C, const float* work, size_t work_floats) {
+  return !ta && (beta == 0.f || beta == 1.f) && panel_shape(N, K) && panel_mode() != 0 &&
+         lda == K && ldc == N && work && work_floats >= (size_t)(K * N) &&
+         ((uintptr_t)A & 15) == 0 && ((uintptr_t)C & 15) == 0 && ((uintptr_t)work & 15) == 0;
+}
+
+static int tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                   const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
+                   size_t work_floats, hipStream_t stream, const float* Cin,
+                   const float* bias = nullptr, int64_t brows = 0);
+
 int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                  const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
                  size_t work_floats, hipStream_t stream) {
+  return tt_gemm(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, beta, work, work_floats, stream, C);
+}
+
+extern "C" int pntf_tt_act_fwd_biased(int ndir, int nl, const float* y, float* h, int64_t m,
+                                      int w, hipStream_t stream);
+
+// Cin != C (and a bias) only on the LDS panel path (the caller checks panel_path and
+// panel_mode): C = A·op(B) (+ bias on rows < brows) + Cin
+static int tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                   const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
+                   size_t work_floats, hipStream_t stream, const float* Cin, const float* bias,
+                   int64_t brows) {
   if (M < 0 || N < 0 || K < 0 || N % BN != 0) {
     snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: need M, K >= 0 and N a multiple of %d", BN);
     return PNTF_ERR_ARG;
@@ -1291,13 +1327,11 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
     snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: null pointer");
     return PNTF_ERR_ARG;
   }
-  if (!ta && (beta == 0.f || beta == 1.f) && panel_shape(N, K) && panel_mode() != 0 &&
-      lda == K && ldc == N && work && work_floats >= (size_t)(K * N) &&
-      ((uintptr_t)A & 15) == 0 && ((uintptr_t)C & 15) == 0 && ((uintptr_t)work & 15) == 0) {
+  if (panel_path(ta, N, K, lda, ldc, beta, A, C, work, work_floats)) {
     const int64_t nf = (N / 32) * (K / 8) * 64;
     hipLaunchKernelGGL(panel_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0,
                        stream, B, ldb, tb, (int)K, (int)N, reinterpret_cast<f32x4*>(work));
-    PanelArgs p{A, reinterpret_cast<const f32x4*>(work), C, M, lda, ldc};
+    PanelArgs p{A, reinterpret_cast<const f32x4*>(work), C, M, lda, ldc, Cin, bias, brows};
     const int64_t tiles = (M + 31) / 32, wgs = (tiles + 3) / 4;
     if (panel_mode() == 2) {
       // one workgroup per CU (128 KiB of LDS at K = 256); per group at most CUs / NG of them
@@ -1457,6 +1491,14 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
   const bool fused = schedule == 1 || schedule == 3 ||
                      (schedule == 0 && rounds >= 3 && 10 * blocks >= 9 * rounds * waves);
   if (!fused) {
+    // the residual enters the GEMM's epilogue (y = x·Wᵀ + res, its C read 4 iterations ahead),
+    // so the act pass reads y and writes h instead of reading y and res and writing both back
+    if (res && nl > 0 && panel_mode() == 2 && panel_path(0, n, k, k, n, 1.f, x, y, work, work_floats)) {
+      int st = tt_gemm(0, 1, R * m, n, k, x, k, W, k, y, n, 1.f, work, work_floats, stream, res,
+                       bias, m);
+      if (st) return st;
+      return pntf_tt_act_fwd_biased(ndir, nl, y, h, m, n, stream);
+    }
     int st = pntf_tt_gemm(0, 1, R * m, n, k, x, k, W, k, y, n, 0.f, work, work_floats, stream);
     if (st) return st;
     return pntf_tt_act_fwd(ndir, nl, y, h, bias, res, m, n, act, stream);

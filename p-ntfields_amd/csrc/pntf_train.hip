@@ -125,7 +125,9 @@ __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) 
 // (σ = σ(10y), σ' = 10σ(1-σ); summed row l covers the J rows k of its endpoint group,
 // l·NDIR/NL <= k < (l+1)·NDIR/NL).  RES: the residual branch (:744, :828) res (R, M, W) is
 // added to every plane first (and the sum kept in y).
-template <int NDIR, int NL, bool ACT, bool RES>
+// BIAS = false: y already holds bias + residual (the panel GEMM's epilogue added them,
+// pntf_gemm.hip tt_linear_res); only h is written.
+template <int NDIR, int NL, bool ACT, bool RES, bool BIAS = true>
 __global__ __launch_bounds__(256) void tt_act_fwd_kernel(float* __restrict__ y, float* __restrict__ h,
                                   const float* __restrict__ bias, const float* __restrict__ res,
                                   int64_t M, int W) {
@@ -133,9 +135,12 @@ __global__ __launch_bounds__(256) void tt_act_fwd_kernel(float* __restrict__ y, 
   const int64_t plane = M * W;
   for (int64_t i = 4 * (blockIdx.x * (int64_t)blockDim.x + threadIdx.x); i < plane;
        i += 4 * (int64_t)gridDim.x * blockDim.x) {
-    f4 v = ld4(y + i) + ld4(bias + i % W);
-    if (RES) v += ld4(res + i);
-    st4(y + i, v);
+    f4 v = ld4(y + i);
+    if (BIAS) {
+      v += ld4(bias + i % W);
+      if (RES) v += ld4(res + i);
+      st4(y + i, v);
+    }
     if (!ACT) continue;
     f4 s, ds, hv;
 #pragma unroll
@@ -650,6 +655,26 @@ int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, con
   }
 #undef PNTF_ACT_FWD
   return check_launch("tt_act_fwd_kernel");
+}
+
+// act pass of a Linear whose panel GEMM already added bias and residual (pntf_gemm.hip):
+// reads y, writes h.  Library-internal (not in include/pntf.h).
+extern "C" __attribute__((visibility("hidden"))) int pntf_tt_act_fwd_biased(
+    int ndir, int nl, const float* y, float* h, int64_t m, int w, hipStream_t stream) {
+  const bool shape = (nl == 1 && (ndir == 3 || ndir == 6)) || (nl == 2 && (ndir == 6 || ndir == 12));
+  if (!shape || m < 0 || (w != 128 && w != 256) || (m > 0 && (!y || !h)))
+    return fail("pntf_tt_act_fwd_biased: bad arguments");
+  if (m == 0) return PNTF_OK;
+  const dim3 g(grid_1d(m * w / 4)), b(256);
+  float* yy = const_cast<float*>(y);
+  if (nl == 1) {
+    if (ndir == 3) hipLaunchKernelGGL((tt_act_fwd_kernel<3, 1, true, false, false>), g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
+    else hipLaunchKernelGGL((tt_act_fwd_kernel<6, 1, true, false, false>), g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
+  } else {
+    if (ndir == 6) hipLaunchKernelGGL((tt_act_fwd_kernel<6, 2, true, false, false>), g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
+    else hipLaunchKernelGGL((tt_act_fwd_kernel<12, 2, true, false, false>), g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
+  }
+  return check_launch("tt_act_fwd_kernel<biased>");
 }
 
 int pntf_tt_act_bwd(int ndir, int nl, const float* y, float* g, int64_t m, int w, int act,

@@ -35,13 +35,18 @@ from . import _lib, ops
 from ._lib import PntfError, check
 
 H = 128
-# Schedule of the forward Linear + act (pntf_tt_linear_act): 0 AUTO (the fused kernel where its
-# 32-point blocks balance over the waves), 1 always fused, 2 always pntf_tt_gemm +
-# pntf_tt_act_fwd (the y planes round-trip HBM).  PNTF_TT_FUSED sets it (to compare).
-_LINEAR_ACT = int(os.environ.get("PNTF_TT_FUSED", "0"))
+# Schedule of the forward Linear + act (pntf_tt_linear_act): 2 (default) the LDS panel GEMM
+# (with bias and residual in its epilogue on residual layers) + the act pass; 0 the library's
+# AUTO, 1 / 3 the fused kernels (one / four waves per 32-point block).  PNTF_TT_FUSED sets it
+# (to compare; profiles/r04_train_sched*.txt).
+_LINEAR_ACT = int(os.environ.get("PNTF_TT_FUSED", "2"))
 # Input gradient + the previous layer's act adjoint in one kernel (pntf_tt_linear_bwd): 1, or
-# pntf_tt_gemm then pntf_tt_act_bwd: 0.  PNTF_TT_BWD sets it (to compare).
-_LINEAR_BWD = int(os.environ.get("PNTF_TT_BWD", "0"))
+# pntf_tt_gemm then pntf_tt_act_bwd: 0; unset (None): the fused kernel for layers of at least
+# _BWD_FUSED_MIN_POINTS points (it balances only with several blocks per wave: 2 x 100 000
+# pairs 64.9 -> 63.3 ms, 2 x 10 000 6.86 -> 7.08 ms).  PNTF_TT_BWD sets it.
+_LINEAR_BWD = (int(os.environ["PNTF_TT_BWD"]) if os.environ.get("PNTF_TT_BWD", "") != ""
+               else None)
+_BWD_FUSED_MIN_POINTS = 100000
 _BLOCK_HEADS = ("encoder.1", "encoder.2", "generator.0", "generator.1", "generator.2")
 
 
@@ -216,7 +221,8 @@ def _adjoint(tape, g, grads, part, merge_bwd):
         W = params[name + ".weight"]
         prev = order[idx + 1]
         res = pending.pop() if name in _BLOCK_HEADS else None
-        fused_in = bool(_LINEAR_BWD) and name != "generator.0" and prev[3]
+        use_bwd = (M >= _BWD_FUSED_MIN_POINTS) if _LINEAR_BWD is None else bool(_LINEAR_BWD)
+        fused_in = use_bwd and name != "generator.0" and prev[3]
         if fused_in:
             # gx = act_bwd_prev(g·W (+ res)): in place into the residual branch's buffer
             gx = res if res is not None else torch.empty((R, M, K), dtype=torch.float32,

@@ -36,7 +36,8 @@ def main(reps=10):
             loss.backward()
             opt.step()
             opt.zero_grad()
-        for sched, bwd in ((0, 0), (2, 0), (1, 0), (3, 0), (3, 1), (2, 1), (0, 0)):
+        defaults = (train._LINEAR_ACT, train._LINEAR_BWD)
+        for sched, bwd in (defaults, (0, 0), (2, 0), (1, 0), (3, 0), (3, 1), (2, 1), defaults):
             train._LINEAR_ACT = sched
             train._LINEAR_BWD = bwd
             step()
@@ -46,8 +47,8 @@ def main(reps=10):
                 step()
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / reps * 1e3
-            print("train step %dx%d  linear_act schedule %d, fused bwd %d: %.3f ms"
-                  % (E, n, sched, bwd, ms), flush=True)
+            print("train step %dx%d  linear_act schedule %d, fused bwd %s: %.3f ms"
+                  % (E, n, sched, "auto" if bwd is None else bwd, ms), flush=True)
 
 
 if __name__ == "__main__":

@@ -498,10 +498,12 @@ TRAIN_FLOP_PER_PAIR = 3 * 14_286_848
 TRAIN_FLOP_EXECUTED_PER_PAIR = 3 * 2 * (2 * 5 * 114_688 + 9 * 425_984)
 
 
-def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=5):
+def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=20, warm=5):
     """Model.train inner step (model_res_sigmoid_multi.py:1040-1052) on the HIP Taylor tape:
     Loss forward + loss.backward() + AdamW step.  (2, 10000) is the reference's batch
-    (Batch Size 2 environments x inner_batch 10000 pairs, :1010-1036)."""
+    (Batch Size 2 environments x inner_batch 10000 pairs, :1010-1036).  `warm` untimed steps
+    first: after the host syncs of the legs before it the GPU clock ramps back over the first
+    few launches, which one warm-up step of ~160 launches does not cover."""
     from models import model_res_sigmoid_multi as md
     from pntf import synth
     from pntf.train import AdamW
@@ -523,7 +525,8 @@ def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=5):
             loss.backward()
             opt.step()
             opt.zero_grad()
-        step()
+        for _ in range(warm):
+            step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):

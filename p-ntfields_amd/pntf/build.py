@@ -95,15 +95,20 @@ def scratch_policy_violations(asm):
     tile and its stores do not refresh the CU's vector L1, so every load through the scratch
     descriptor (the one the nt stores use) must carry the nt policy (bypass L1).  Returns
     (scratch descriptors, nt loads through them, loads through them without nt)."""
-    descs = set(SCRATCH_STORE.findall(asm))
-    good = bad = 0
-    for m in BUFFER_LOAD.finditer(asm):
-        if m.group(1) in descs:
-            if re.search(r"\bnt\b", m.group(2)):
-                good += 1
-            else:
-                bad += 1
-    return descs, good, bad
+    # per kernel: a unit may hold several instantiations (wide_field_kernel<DIM, KIND, BL>),
+    # whose register allocations can give the scratch and weight descriptors each other's SGPRs
+    bodies = [b for b in re.split(r"(?m)^(?=_Z\w+:)", asm) if b.startswith("_Z")] or [asm]
+    descs_all, good, bad = set(), 0, 0
+    for body in bodies:
+        descs = set(SCRATCH_STORE.findall(body))
+        descs_all |= descs
+        for m in BUFFER_LOAD.finditer(body):
+            if m.group(1) in descs:
+                if re.search(r"\bnt\b", m.group(2)):
+                    good += 1
+                else:
+                    bad += 1
+    return descs_all, good, bad
 
 # units whose kernels must not spill SGPRs either: the headline τ+∇τ kernel and its τ-only /
 # travel-time siblings (the narrow 16-pair kernels still spill ~24-335 SGPRs to VGPR lanes)

@@ -32,7 +32,7 @@ __global__ void pack_kernel(const float* __restrict__ src, int rows, int cols, i
                             int trans, float* __restrict__ dst);
 __global__ void copy_kernel(const float* __restrict__ src, int n, float* __restrict__ dst);
 __global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int cols, int ld,
-                                 int trans, float* __restrict__ dst);
+                                 int trans, float scale, float* __restrict__ dst);
 __global__ void pack_wide_aux_kernel(const float* __restrict__ plain, float* __restrict__ wide);
 __global__ void pack_quad_kernel(const float* __restrict__ src, int rows, int cols, int dir,
                                  float* __restrict__ dst);
@@ -342,10 +342,12 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
     hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx], d.cols,
                        d.rows, d.cols, 1, packed + OFF_BWD + d.off);
     // the wide (32x32x2) fragment order of the same two matrices
+    // (forward encoder[0] times κ: the wide kernels carry κ-scaled activations, pntf_wide.h)
     hipLaunchKernelGGL(pack_wide_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx],
-                       d.rows, d.cols, d.cols, 0, packed + OFF_WIDE + OFF_FWD + d.off);
+                       d.rows, d.cols, d.cols, 0, d.off == OFF_E0 ? WIDE_KAPPA : 1.f,
+                       packed + OFF_WIDE + OFF_FWD + d.off);
     hipLaunchKernelGGL(pack_wide_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx],
-                       d.cols, d.rows, d.cols, 1, packed + OFF_WIDE + OFF_BWD + d.off);
+                       d.cols, d.rows, d.cols, 1, 1.f, packed + OFF_WIDE + OFF_BWD + d.off);
   }
   // the quad streams: every layer of both directions in planner-step order
   for (int L = 0; L < Q_NL; ++L) {

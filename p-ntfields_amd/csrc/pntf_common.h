@@ -89,6 +89,9 @@ static_assert(Q_WAVES == 4 || Q_WAVES == 8, "quad layers: 4 or 8 waves per workg
 constexpr int Q_NL = 26;
 constexpr int Q_STREAM = 2 * SZ_DIR / Q_WAVES;      // floats of one wave's fragment stream
 constexpr int Q_NF_FWD = SZ_DIR / Q_WAVES / 256;    // 1 KiB fragments of its forward part
+// the wide kernels carry their activations times 10 / ln 2 (pntf_wide.h WKAPPA; the packer
+// scales encoder[0]'s forward fragments and the forward bias columns by it)
+constexpr float WIDE_KAPPA = 14.4269504088896341f;
 // env-B table staged in LDS by the wide kernels when n_env · dim · 128 floats fit (pntf_wide.h
 // WBt<true>): 20 KiB, i.e. dim 3 up to 13 environments, dim 6 up to 6
 constexpr int WBL_FLOATS = 5120;

@@ -336,21 +336,27 @@ def run(args):
     return 0
 
 
-def _timeit(fn, reps=5, warm=1):
-    """Mean time of `reps` back-to-back calls after `warm` untimed ones.  After any idle gap
-    the GPU's clocks ramp back over ~5 launches (profiles/r04_c2_launches.txt: 6.3 -> 5.2 ms
-    for the 262 144-pair kernel), so short kernels get a longer warm-up."""
+def _timeit(fn, reps=5, warm=1, stats=False):
+    """Time `reps` back-to-back calls after `warm` untimed ones, one HIP event pair per call on
+    the launch stream.  Returns the mean (ms), or with `stats` {"mean", "median", "min", "max",
+    "reps", "warm"}.  After any idle gap the GPU's clocks ramp back over ~5 launches
+    (profiles/r04_c2_launches.txt: 6.3 -> 5.2 ms for the 262 144-pair kernel), so every leg
+    warms up with >= 5 calls and reports the median and the minimum as well."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
-    a = torch.cuda.Event(enable_timing=True)
-    b = torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for a, b in evs:
+        a.record()
         fn()
-    b.record()
+        b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps
+    ts = np.array([a.elapsed_time(b) for a, b in evs])
+    if not stats:
+        return float(ts.mean())
+    return {"mean": float(ts.mean()), "median": float(np.median(ts)), "min": float(ts.min()),
+            "max": float(ts.max()), "reps": reps, "warm": warm}
 
 
 def sharded_extras(packed, dev, rank, ws, q=1024):
@@ -378,8 +384,9 @@ def sharded_extras(packed, dev, rank, ws, q=1024):
         gather()
 
     el = timed(run, 3, 1, ws, torch.cuda.synchronize, dev)
-    mine = torch.tensor([_timeit(plan, reps=3), _timeit(gather, reps=3)], dtype=torch.float64,
-                        device=dev)
+    mine = torch.tensor([_timeit(plan, reps=10, warm=5, stats=True)["median"],
+                         _timeit(gather, reps=10, warm=2, stats=True)["median"]],
+                        dtype=torch.float64, device=dev)
     every = [torch.zeros_like(mine) for _ in range(ws)]
     tdist.all_gather(every, mine)
     every = torch.stack(every).cpu().numpy()
@@ -410,7 +417,7 @@ def extras(packed, dev):
     Bh = torch.from_numpy(synth.make_B_table(10, 3)).to(dev)
     eh = torch.from_numpy(synth.make_env_ids(n1, 10)).to(dev)
     out["headline_1M_wave_tile_kernel_ms"] = timeit(
-        lambda: ops.tau_grad(packed, xh, Bh, eh, dim=3, schedule="wave_tile"), reps=3)
+        lambda: ops.tau_grad(packed, xh, Bh, eh, dim=3, schedule="wave_tile"), reps=3, warm=3)
     del xh, eh
     # C1 shape on the GPU (4096 pairs, latency-bound): split tiles vs one wave per tile
     x1 = torch.from_numpy(synth.make_pairs(4096, 3, seed=2)).to(dev)
@@ -423,8 +430,10 @@ def extras(packed, dev):
     B3 = torch.from_numpy(synth.make_B_table(10, 3)).to(dev)
     e3 = torch.from_numpy(synth.make_env_ids(n3, 10)).to(dev)
     y3 = torch.from_numpy(synth.make_speeds(n3)).to(dev)
-    ms = timeit(lambda: ops.eikonal_residual(packed, x3, B3, e3, 3, yobs=y3, gamma=1e-3),
-                reps=3)
+    st = timeit(lambda: ops.eikonal_residual(packed, x3, B3, e3, 3, yobs=y3, gamma=1e-3),
+                reps=10, warm=5, stats=True)
+    ms = st["median"]
+    out["c3_eikonal_residual_1M_ms"] = st
     out["c3_eikonal_residual_1M_pairs_per_s"] = n3 / (ms * 1e-3)
     out["c3_eikonal_residual_TFLOPs"] = 14_286_848 * n3 / (ms * 1e-3) / 1e12
     # C5: UR5 arm, 1024 queries, <= 200 steps, per-query freeze
@@ -436,15 +445,20 @@ def extras(packed, dev):
     def run_plan(schedule):
         res["p"] = ops.plan(packed, xq, Ba, dim=6, step=0.015, tol=0.03, max_iter=199,
                             mode=ops.GRAD_EXACT, schedule=schedule)
-    ms = timeit(lambda: run_plan("auto"), reps=2)
+    st = timeit(lambda: run_plan("auto"), reps=10, warm=5, stats=True)
+    ms = st["median"]
     steps = res["p"][1].cpu().numpy()
-    out["c5_arm_plan_1024q_ms"] = ms
+    out["c5_arm_plan_1024q_ms"] = ms                   # median of 10 after 5 warm-up plans
+    out["c5_arm_plan_1024q_ms_min"] = st["min"]
+    out["c5_arm_plan_1024q_ms_stats"] = st
     out["c5_arm_plan_query_steps_per_s"] = float(steps.sum()) / (ms * 1e-3)
     out["c5_arm_plan_mean_steps"] = float(steps.mean())
     out["c5_arm_plan_max_steps"] = int(steps.max())
     out["c5_arm_plan_handoffs"] = ops.plan_handoff_counts(dev)[1]   # 0 = no tail hand-off
-    out["c5_arm_plan_1024q_wave_tile_ms"] = timeit(lambda: run_plan("wave_tile"), reps=2)
-    out["c5_arm_plan_1024q_split_tile_ms"] = timeit(lambda: run_plan("split_tile"), reps=2)
+    out["c5_arm_plan_1024q_wave_tile_ms"] = timeit(lambda: run_plan("wave_tile"), reps=5,
+                                                   warm=2, stats=True)["median"]
+    out["c5_arm_plan_1024q_split_tile_ms"] = timeit(lambda: run_plan("split_tile"), reps=10,
+                                                    warm=5, stats=True)["median"]
     # the quad planner's C5 step time and its roofline: a step streams both weight directions
     # (4.33 MB) through each tile's CU; the measured per-CU stream floor is ~33 us with the
     # tile's 8 waves loading (tests/diag/stream_probe2.hip), the 4x4x1 MFMA work ~17 us at the
@@ -468,8 +482,9 @@ def extras(packed, dev):
         def run1():
             res["p1"] = ops.plan(packed, x1, B1, dim=3, step=0.03, tol=1e-9, max_iter=99,
                                  mode=ops.GRAD_BACKGRAD_COMPAT, schedule=sched)
-        ms = timeit(run1, reps=2)
-        out["gib_plan_q1_ms_per_step_" + sched] = ms / 100.0
+        st = timeit(run1, reps=10, warm=5, stats=True)
+        out["gib_plan_q1_ms_per_step_" + sched] = st["median"] / 100.0
+        out["gib_plan_q1_ms_per_step_min_" + sched] = st["min"] / 100.0
     out.update(train_extras(dev))
     out.update(mesh_extras(dev))
     return out

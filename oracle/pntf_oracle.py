@@ -461,15 +461,26 @@ def _loss_bwd(xp, yobs, tau, dtau, ltau, dim, gamma, scale, arm):
     return diff, gt, gd, gl
 
 
-def eikonal_loss_grad(params, xp, yobs, B, env=None, dim=3, gamma=1e-3, scale=1.0, arm=False,
-                      dtype=np.float64):
-    """Weight gradients of scale·Σ_pairs diff — loss.backward() of Model.Loss with
-    scale = beta/(E·n) (multi, :947-948) or beta/N (arm).  The B regulariser of loss_n has no
-    weight gradient.  Returns (diff (N,), grads {state-dict key: array}); encoder1.0 gets none
-    (created :160 but never used)."""
-    p = cast_params(params, dtype)
-    xp = np.asarray(xp, dtype=dtype)
-    yobs = np.asarray(yobs, dtype=dtype)
+def _tact_q(y, J, L):
+    """encoder[0]'s act in NN.out_backgrad (model_res_sigmoid_multi.py:435-438): the
+    derivative row is multiplied by σ(10·softplus(y)) instead of σ(10y); first order only."""
+    h = softplus10(y)
+    return h, J * sig10(h)[:, None], np.zeros_like(L)
+
+
+def _tact_q_bwd(y, J, L, gh, gJ, gL):
+    """Adjoint of _tact_q: d σ(10 sp(y)) / dy = 10 σq (1 - σq) σ(10y)."""
+    s = sig10(y)
+    sq = sig10(softplus10(y))
+    dq = SCALE * sq * (1.0 - sq) * s
+    gy = gh * s + np.sum(gJ * J * dq[:, None], axis=1)
+    return gy, gJ * sq[:, None], np.zeros_like(gL)
+
+
+def _taylor_tape(p, xp, B, env, dim, dtype, compat=False):
+    """Taylor-mode forward of NN.out_laplace (model_res_sigmoid_multi.py:710-848; arm
+    models/model_res_sigmoid.py:676-826) with every Linear input and pre-activation kept for
+    the reverse sweep.  compat: encoder[0]'s J row uses the out_backgrad quirk (_tact_q)."""
     n = xp.shape[0]
     w, per = _per_point_W(B, env, n, dtype)
     ww = np.concatenate([w, w]) if per else w
@@ -486,11 +497,11 @@ def eikonal_loss_grad(params, xp, yobs, B, env=None, dim=3, gamma=1e-3, scale=1.
         tape.append(("lin", name, t3, res is not None))
         return out
 
-    def act(y3):
-        tape.append(("act", y3))
-        return _taylor_act(*y3)
+    def act(y3, quirk=False):
+        tape.append(("actq" if quirk else "act", y3))
+        return _tact_q(*y3) if quirk else _taylor_act(*y3)
 
-    h = act(lin(phi, "encoder.0"))
+    h = act(lin(phi, "encoder.0"), quirk=compat)
     for i in (1, 2):
         a = act(lin(h, "encoder.%d" % i))
         h = act(lin(a, "encoder1.%d" % i, res=h))
@@ -510,23 +521,44 @@ def eikonal_loss_grad(params, xp, yobs, B, env=None, dim=3, gamma=1e-3, scale=1.
         u3 = act(lin(a, "generator1.%d" % i, res=u3))
     v3 = act(lin(u3, "generator.3"))
     y, Jy, Ly = lin(v3, "generator.4")
-    y, Jy, Ly = y[:, 0], Jy[:, :, 0], Ly[:, :, 0]
+    return dict(n=n, dim=dim, tape=tape, y=y[:, 0], Jy=Jy[:, :, 0], Ly=Ly[:, :, 0],
+                merge=(Js, Jg, Ls, Lg, s0), q=q, wd=wd)
+
+
+def _taylor_head(st):
+    """actout_laplace (:693-708): τ (n,1), ∇τ (n,2dim), diagonal ∇²τ (n,2dim) and the
+    derivatives of σ(0.1y) it needs for the adjoint."""
+    y, Jy, Ly = st["y"], st["Jy"], st["Ly"]
     t = sig_out(y)
     dt = 0.1 * t * (1.0 - t)
     ddt = 0.1 * dt * (1.0 - 2.0 * t)
     dddt = 0.1 * (ddt * (1.0 - 2.0 * t) - 2.0 * dt * dt)
-    tau, dtau, ltau = t[:, None], Jy * dt[:, None], Jy * Jy * ddt[:, None] + Ly * dt[:, None]
-    diff, gt, gd, gl = _loss_bwd(xp, yobs, tau, dtau, ltau, dim, gamma, scale, arm)
-    # actout_laplace adjoint
-    g = (gt * dt + np.sum(gd * Jy * ddt[:, None] + gl * (Jy * Jy * dddt[:, None] + Ly * ddt[:, None]), 1),
+    return (t[:, None], Jy * dt[:, None], Jy * Jy * ddt[:, None] + Ly * dt[:, None],
+            (t, dt, ddt, dddt))
+
+
+def _taylor_adjoint(st, p, gt, gd, gl, want_x=False):
+    """Reverse sweep of the Taylor tape from d/d(τ, ∇τ rows, ∇²τ rows): weight gradients of
+    every Linear used and, with want_x, d/dxp through the Fourier features (:199-213)."""
+    dim, n = st["dim"], st["n"]
+    Jy, Ly = st["Jy"], st["Ly"]
+    _, _, _, (t, dt, ddt, dddt) = _taylor_head(st)
+    g = (gt * dt + np.sum(gd * Jy * ddt[:, None]
+                          + gl * (Jy * Jy * dddt[:, None] + Ly * ddt[:, None]), 1),
          gd * dt[:, None] + 2.0 * gl * Jy * ddt[:, None], gl * dt[:, None])
     g = (g[0][:, None], g[1][:, :, None], g[2][:, :, None])
+    Js, Jg, Ls, Lg, s0 = st["merge"]
+    s1 = 1.0 - s0
+    c = SCALE * s0 * s1
+    S0, S1, C = s0[:, None], s1[:, None], c[:, None]
     grads = {}
     res_pending = []
-    gz = None
-    for op in reversed(tape):
+    for op in reversed(st["tape"]):
         if op[0] == "act":
             g = _tact_bwd(*op[1], *g)
+            continue
+        if op[0] == "actq":
+            g = _tact_q_bwd(*op[1], *g)
             continue
         _, name, x3, has_res = op
         gin = _tlin_bwd(*x3, p[name + ".weight"], *g, grads, name)
@@ -552,6 +584,58 @@ def eikonal_loss_grad(params, xp, yobs, B, env=None, dim=3, gamma=1e-3, scale=1.
             gLs, gLg = gLsM * S0 + gLsm * S1, gLgM * S1 + gLgm * S0
             g = (np.concatenate([gzs, gzg]), np.concatenate([gJs, gJg]),
                  np.concatenate([gLs, gLg]))
+    if not want_x:
+        return grads, None
+    # Fourier adjoint: Φ = [sin q | cos q], J_k = w_k [cos q | -sin q], L_k = -w_k² [sin q | cos q]
+    gh, gJ, gL = g
+    q, wd = st["q"], st["wd"]
+    sq, cq = np.sin(q), np.cos(q)
+    G = gh[:, :H] * cq - gh[:, H:] * sq
+    G = G - np.sum(wd * (gJ[:, :, :H] * sq[:, None] + gJ[:, :, H:] * cq[:, None]), 1)
+    G = G + np.sum(wd * wd * (-gL[:, :, :H] * cq[:, None] + gL[:, :, H:] * sq[:, None]), 1)
+    gx = np.einsum("mj,mdj->md", G, wd)
+    return grads, np.concatenate([gx[:n], gx[n:]], axis=1)
+
+
+def taylor_vjp(params, xp, B, env=None, dim=3, g_tau=None, g_dtau=None, g_ltau=None,
+               compat=False, want_x=True, dtype=np.float64):
+    """Vector-Jacobian product of NN.out_laplace's outputs (models/model_res_sigmoid_multi.py:
+    710-848; arm models/model_res_sigmoid.py:676-826), of NN.out_grad's (:303-400) and, with
+    compat, of NN.out_backgrad's (:402-647, encoder[0] quirk :435-438; first order only):
+    the gradients that `(Σ g_tau·τ + Σ g_dtau·∇τ + Σ g_ltau·∇²τ).backward()` leaves on every
+    trained parameter and on the coordinates in the reference's autograd graph.
+    g_tau (n,), g_dtau (n, 2dim), g_ltau (n, 2dim) or None (zero).  Returns
+    ((τ (n,1), ∇τ (n,2dim), ∇²τ (n,2dim)), grads {key: array}, dcoords (n, 2dim) or None);
+    encoder1.0 (never used, :160) gets no entry."""
+    p = cast_params(params, dtype)
+    xp = np.asarray(xp, dtype=dtype)
+    n = xp.shape[0]
+    if compat and g_ltau is not None:
+        raise ValueError("out_backgrad has no second-derivative output")
+    st = _taylor_tape(p, xp, B, env, dim, dtype, compat=compat)
+    tau, dtau, ltau, _ = _taylor_head(st)
+    z1 = np.zeros(n, dtype)
+    z2 = np.zeros((n, 2 * dim), dtype)
+    gt = z1 if g_tau is None else np.asarray(g_tau, dtype).reshape(n)
+    gd = z2 if g_dtau is None else np.asarray(g_dtau, dtype).reshape(n, 2 * dim)
+    gl = z2 if g_ltau is None else np.asarray(g_ltau, dtype).reshape(n, 2 * dim)
+    grads, dx = _taylor_adjoint(st, p, gt, gd, gl, want_x)
+    return (tau, dtau, ltau), grads, dx
+
+
+def eikonal_loss_grad(params, xp, yobs, B, env=None, dim=3, gamma=1e-3, scale=1.0, arm=False,
+                      dtype=np.float64):
+    """Weight gradients of scale·Σ_pairs diff — loss.backward() of Model.Loss with
+    scale = beta/(E·n) (multi, :947-948) or beta/N (arm).  The B regulariser of loss_n has no
+    weight gradient.  Returns (diff (N,), grads {state-dict key: array}); encoder1.0 gets none
+    (created :160 but never used)."""
+    p = cast_params(params, dtype)
+    xp = np.asarray(xp, dtype=dtype)
+    yobs = np.asarray(yobs, dtype=dtype)
+    st = _taylor_tape(p, xp, B, env, dim, dtype)
+    tau, dtau, ltau, _ = _taylor_head(st)
+    diff, gt, gd, gl = _loss_bwd(xp, yobs, tau, dtau, ltau, dim, gamma, scale, arm)
+    grads, _ = _taylor_adjoint(st, p, gt, gd, gl)
     return diff, grads
 
 

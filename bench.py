@@ -359,6 +359,18 @@ def _timeit(fn, reps=5, warm=1, stats=False):
             "max": float(ts.max()), "reps": reps, "warm": warm}
 
 
+def shard_gather_plans(plan_local, xq_all, rank, ws):
+    """The sharded planner exchange of SURVEY.md §8e: rank `rank` of `ws` plans its contiguous
+    shard_range of the queries with plan_local(xq_shard) -> (path (q_r, T, 2dim), steps
+    (q_r,)) and every rank receives all paths and step counts in query order (the all-gather
+    of dist.all_gather_rows; uneven shards padded inside it).  bench.py's sharded C5 extra
+    and the 8-rank CPU rehearsal (tests/test_dist.py) both go through here."""
+    q = xq_all.shape[0]
+    lo, hi = dist.shard_range(q, rank, ws)
+    path, steps = plan_local(xq_all[lo:hi])
+    return dist.all_gather_rows(path, q), dist.all_gather_rows(steps, q)
+
+
 def sharded_extras(packed, dev, rank, ws, q=1024):
     """N > 1: the C5 arm planner with its 1024 queries sharded over the ranks, then the RCCL
     all-gather of every rank's paths (the planner-path exchange of SURVEY.md §8e); the wall
@@ -380,8 +392,10 @@ def sharded_extras(packed, dev, rank, ws, q=1024):
         res["steps"] = dist.all_gather_rows(steps, q)
 
     def run():
-        plan()
-        gather()
+        res["paths"], res["steps"] = shard_gather_plans(
+            lambda x: ops.plan(packed, torch.from_numpy(x.copy()).to(dev), Ba, dim=6,
+                               step=0.015, tol=0.03, max_iter=199, mode=ops.GRAD_EXACT),
+            xq_all, rank, ws)
 
     el = timed(run, 3, 1, ws, torch.cuda.synchronize, dev)
     mine = torch.tensor([_timeit(plan, reps=10, warm=5, stats=True)["median"],

@@ -205,9 +205,14 @@ int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, cons
                     int32_t n_env, float* phi, hipStream_t stream);
 
 /* Bias (+ residual) + act_laplace (:663-691, residual :744/:828) on GEMM output y (R, m, w),
- * w = 128|256, (ndir, nl) = (3|6, 1), (6|12, 2) or (0, 0) (value plane only): y's value plane += bias, every plane += res
- * (R, m, w) when res is not NULL (y is kept as the tape); act != 0: h (R, m, w) = softplus10
- * Taylor rows.  act == 0 (Linear without activation, res must be NULL): bias only, h unused. */
+ * w = 128|256, (ndir, nl) = (3|6, 1), (6|12, 2) (summed second derivatives), (0, 0) (value
+ * plane only), (3|6|12, 0) (first derivatives only) or (3, 3), (6, 6), (12, 12) (one
+ * second-derivative row per direction; the general VJP tape below): y's value plane += bias,
+ * every plane += res (R, m, w) when res is not NULL (y is kept as the tape); act == 1: h (R, m,
+ * w) = softplus10 Taylor rows; act == 2 (nl == 0, ndir 3|6, encoder[0] of NN.out_backgrad):
+ * the derivative rows are multiplied by σ(10·softplus(y)) instead of σ(10y), the reference's
+ * quirk (:435-438).  act == 0 (Linear without activation, res must be NULL): bias only, h
+ * unused. */
 int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, const float* res,
                     int64_t m, int w, int act, hipStream_t stream);
 
@@ -223,6 +228,36 @@ int pntf_tt_act_bwd(int ndir, int nl, const float* y, float* g, int64_t m, int w
 int pntf_tt_merge_fwd(int dim, const float* z, int64_t n, float* u, hipStream_t stream);
 int pntf_tt_merge_bwd(int dim, const float* z, const float* gu, int64_t n, float* gz,
                       hipStream_t stream);
+
+/* ---- General VJP tape (round 5): the backward of a loss a user writes on NN.out_laplace's
+ * (τ, ∇τ, diagonal ∇²τ) (:710-848), NN.out_grad's / out_backgrad's (τ, ∇τ) (:303-400,
+ * :402-647) or Model.gradient's ∇τ with create_graph (:890-896), w.r.t. every weight and the
+ * coordinates — what the reference's autograd computes through those plain torch graphs.
+ * Encoder planes (ndir, nl) = (0, 0), (dim, 0), (dim, 1) or (dim, dim); nle = the encoder's nl
+ * (0, 1 = per-endpoint sums, dim = per direction); after the merge (2·ndir, 2·nle). */
+/* input_mapping / _grad / _laplace (:186-213): phi (1 + ndir + nl, 2n, 256). */
+int pntf_tt_fourier_ex(int dim, int ndir, int nl, const float* xp, int64_t n, const float* Btab,
+                       const int32_t* env, int32_t n_env, float* phi, hipStream_t stream);
+/* Its adjoint, the coordinates' gradient: gphi (1 + ndir + nl, 2n, 256) = dL/dphi ->
+ * gx (n, 2*dim) = dL/dxp (written). */
+int pntf_tt_fourier_bwd(int dim, int ndir, int nl, const float* gphi, const float* xp, int64_t n,
+                        const float* Btab, const int32_t* env, int32_t n_env, float* gx,
+                        hipStream_t stream);
+/* Start/goal merge (:755-811) for nle second-derivative rows per endpoint: z (1 + dim + nle,
+ * 2n, 128) -> u (1 + 2 dim + 2 nle, n, 256); and its adjoint gu -> gz. */
+int pntf_tt_merge_fwd_ex(int dim, int nle, const float* z, int64_t n, float* u,
+                         hipStream_t stream);
+int pntf_tt_merge_bwd_ex(int dim, int nle, const float* z, const float* gu, int64_t n, float* gz,
+                         hipStream_t stream);
+/* generator[4] + actout_laplace (:693-708) with a general upstream gradient: v (1 + 2 dim +
+ * 2 nle, n, 128) generator[3] output planes -> (each optional) tau (n), dtau (n, 2 dim), lap
+ * (n, 2 nle) (per direction for nle == dim, per-endpoint Laplacian for nle == 1); with the
+ * upstream gtau (n), gdtau (n, 2 dim), glap (n, 2 nle) (NULL = zero): gv (same shape as v),
+ * gw4 (128), gb4 (1) of Σ gtau·τ + gdtau·∇τ + glap·lap. */
+int pntf_tt_head_vjp(int dim, int nle, const float* v, const float* w4, const float* b4,
+                     int64_t n, const float* gtau, const float* gdtau, const float* glap,
+                     float* tau, float* dtau, float* lap, float* gv, float* gw4, float* gb4,
+                     float* partial, hipStream_t stream);
 
 /* ---- First-order (value-plane) tape: the weight gradient of a loss on NN.out's τ
  * (models/model_res_sigmoid_multi.py:215-259, arm models/model_res_sigmoid.py:212-256: plain

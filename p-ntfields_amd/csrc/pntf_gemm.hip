@@ -1457,11 +1457,16 @@ static int tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float*
   return PNTF_OK;
 }
 
+extern "C" int pntf_tt_planes_ok(int ndir, int nl);
+
 int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const float* W,
                        int n, const float* bias, const float* res, float* y, float* h, int act,
                        int schedule, float* work, size_t work_floats, hipStream_t stream) {
-  const bool planes = (nl == 0 && ndir == 0) || (nl == 1 && (ndir == 3 || ndir == 6)) ||
-                      (nl == 2 && (ndir == 6 || ndir == 12));
+  // the fused kernels take the Loss / value tapes' layouts; the first-order and per-direction
+  // layouts of the general VJP tape (and act = 2, the out_backgrad quirk) run the GEMM + act pair
+  const bool basic = ((nl == 0 && ndir == 0) || (nl == 1 && (ndir == 3 || ndir == 6)) ||
+                      (nl == 2 && (ndir == 6 || ndir == 12))) && act != 2;
+  const bool planes = pntf_tt_planes_ok(ndir, nl) && act >= 0 && act <= 2;
   const auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   if (!planes || m < 0 || !panel_shape(n, k) || (m > 0 && (!x || !W || !bias || !y || !work ||
       (act && !h))) || (res && !act) || work_floats < (size_t)k * n ||
@@ -1488,12 +1493,13 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
   const int64_t waves = 4 * nwg, rounds = (blocks + waves - 1) / waves;
   // (and only with several rounds per wave: at one round, generator[3] of the reference batch,
   // the fused kernel measured 227 µs against 132 + 56 for the pair, profiles/r04_train_*)
-  const bool fused = schedule == 1 || schedule == 3 ||
-                     (schedule == 0 && rounds >= 3 && 10 * blocks >= 9 * rounds * waves);
+  const bool fused = basic && (schedule == 1 || schedule == 3 ||
+                     (schedule == 0 && rounds >= 3 && 10 * blocks >= 9 * rounds * waves));
   if (!fused) {
     // the residual enters the GEMM's epilogue (y = x·Wᵀ + res, its C read 4 iterations ahead),
     // so the act pass reads y and writes h instead of reading y and res and writing both back
-    if (res && nl > 0 && panel_mode() == 2 && panel_path(0, n, k, k, n, 1.f, x, y, work, work_floats)) {
+    if (res && (nl > 0 || ndir > 0) && panel_mode() == 2 &&
+        panel_path(0, n, k, k, n, 1.f, x, y, work, work_floats)) {
       int st = tt_gemm(0, 1, R * m, n, k, x, k, W, k, y, n, 1.f, work, work_floats, stream, res,
                        bias, m);
       if (st) return st;

@@ -31,9 +31,35 @@
 #include <math.h>
 #include <stdio.h>
 
+#include <type_traits>
+
 #include "pntf.h"
 
 namespace {
+
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+// The Taylor layouts (ndir, nl) of the tapes, R = 1 + ndir + nl planes per point:
+//   (0, 0)                  value only (the weight gradient of a loss on NN.out's τ)
+//   (dim, 0) / (2dim, 0)    + first derivatives (NN.out_grad / out_backgrad, Model.gradient
+//                           with create_graph: a loss on ∇τ)
+//   (dim, 1) / (2dim, 2)    + the per-endpoint SUM of the second derivatives (Model.Loss)
+//   (dim, dim) / (2dim, 2dim) + one second-derivative row per direction (NN.out_laplace's
+//                           diagonal ∇²τ under a general upstream gradient)
+// encoder / after the start-goal merge.  with_planes calls f(IC<ndir>, IC<nl>).
+template <class F>
+bool with_planes(int ndir, int nl, F&& f) {
+#define PNTF_PL(N, L)              \
+  if (ndir == N && nl == L) {      \
+    f(IC<N>{}, IC<L>{});           \
+    return true;                   \
+  }
+  PNTF_PL(0, 0) PNTF_PL(3, 1) PNTF_PL(6, 1) PNTF_PL(6, 2) PNTF_PL(12, 2)
+  PNTF_PL(3, 0) PNTF_PL(6, 0) PNTF_PL(12, 0) PNTF_PL(3, 3) PNTF_PL(6, 6) PNTF_PL(12, 12)
+#undef PNTF_PL
+  return false;
+}
 
 constexpr int H = 128;
 constexpr float SCALE = 10.f;               // Softplus beta (model_res_sigmoid_multi.py:140)
@@ -69,13 +95,16 @@ __device__ __forceinline__ float softplus10(float y) {
 }
 
 // ---------------------------------------------------------------- Φ planes (:199-213)
-// phi (2 + DIM, 2n, 256): point m < n is x_start of pair m, m >= n the x_goal of pair m - n;
-// planes [value | ∂x_d (DIM) | Σ_d ∂²x_d].  FULL = false: the value plane only (input_mapping
-// :186-190, the first-order tape of NN.out's weight gradient).
-template <int DIM, bool FULL = true>
+// phi (1 + NJ + NL, 2n, 256): point m < n is x_start of pair m, m >= n the x_goal of pair
+// m - n; planes [value | ∂x_d (NJ = DIM, or none) | second derivatives: Σ_d ∂²x_d (NL = 1) or
+// ∂²x_d per direction (NL = DIM)].  (NJ, NL) = (0, 0): the value plane only (input_mapping
+// :186-190, the first-order tape of NN.out's weight gradient); (DIM, 0): input_mapping_grad
+// (:192-197).
+template <int DIM, int NJ, int NL>
 __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict__ xp, int64_t n,
                                   const float* __restrict__ Btab, const int32_t* __restrict__ env,
                                   int32_t n_env, float* __restrict__ phi) {
+  static_assert((NJ == 0 && NL == 0) || (NJ == DIM && (NL == 0 || NL == 1 || NL == DIM)), "planes");
   const int64_t M = 2 * n, plane = M * 256;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M * H;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -86,7 +115,7 @@ __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict
     const int e = env ? env[p] : 0;
     float* o = phi + m * 256 + j;
     if (e < 0 || e >= n_env) {
-      for (int r = 0; r < (FULL ? 2 + DIM : 1); ++r) o[r * plane] = o[r * plane + H] = NAN;
+      for (int r = 0; r < 1 + NJ + NL; ++r) o[r * plane] = o[r * plane + H] = NAN;
       continue;
     }
     const float* B = Btab + (int64_t)e * DIM * H + j;
@@ -101,14 +130,83 @@ __global__ __launch_bounds__(256) void tt_fourier_kernel(const float* __restrict
     sincosf(q, &s, &c);
     o[0] = s;
     o[H] = c;
-    if (!FULL) continue;
 #pragma unroll
-    for (int k = 0; k < DIM; ++k) {
+    for (int k = 0; k < NJ; ++k) {
       o[(1 + k) * plane] = w[k] * c;
       o[(1 + k) * plane + H] = -w[k] * s;
     }
-    o[(1 + DIM) * plane] = -w2 * s;
-    o[(1 + DIM) * plane + H] = -w2 * c;
+    if (NL == 1) {
+      o[(1 + NJ) * plane] = -w2 * s;
+      o[(1 + NJ) * plane + H] = -w2 * c;
+    } else if (NL == DIM) {
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        const float wk2 = w[k] * w[k];
+        o[(1 + NJ + k) * plane] = -wk2 * s;
+        o[(1 + NJ + k) * plane + H] = -wk2 * c;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v);
+
+// Fourier adjoint (the coords gradient of every tape): gphi (1 + NJ + NL, 2n, 256) = dL/dΦ
+// planes -> gx (n, 2 DIM) = dL/dxp.  With q_j = x·w_j: Φ = [sin q | cos q],
+// J_k = w_k [cos q | -sin q], L = -w²[sin q | cos q] (summed, w² = Σ_k w_k²) or -w_k²[...] per
+// direction, so dL/dq_j = G_j sums the planes' q-derivatives and dL/dx_d = Σ_j G_j w_dj.  One
+// wave per point (two features per lane, wave sums in a fixed order).
+template <int DIM, int NJ, int NL>
+__global__ __launch_bounds__(256) void tt_fourier_bwd_kernel(
+    const float* __restrict__ gphi, const float* __restrict__ xp, int64_t n,
+    const float* __restrict__ Btab, const int32_t* __restrict__ env, int32_t n_env,
+    float* __restrict__ gx) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t M = 2 * n, plane = M * 256;
+  for (int64_t m = blockIdx.x * 4 + wave; m < M; m += (int64_t)gridDim.x * 4) {
+    const int64_t p = m < n ? m : m - n;
+    const float* x = xp + p * 2 * DIM + (m < n ? 0 : DIM);
+    float* o = gx + p * 2 * DIM + (m < n ? 0 : DIM);
+    const int e = env ? env[p] : 0;
+    if (e < 0 || e >= n_env) {               // wave-uniform
+      if (lane < DIM) o[lane] = NAN;
+      continue;
+    }
+    const float* B = Btab + (int64_t)e * DIM * H;
+    float acc[DIM];
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int j = lane + 64 * half;
+      float w[DIM], q = 0.f, w2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < DIM; ++k) {
+        w[k] = TWO_PI * B[k * H + j];
+        q = fmaf(x[k], w[k], q);
+        w2 = fmaf(w[k], w[k], w2);
+      }
+      float s, c;
+      sincosf(q, &s, &c);
+      const float* g = gphi + m * 256 + j;
+      float G = g[0] * c - g[H] * s;
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) G -= w[k] * (g[(1 + k) * plane] * s + g[(1 + k) * plane + H] * c);
+      if (NL == 1) {
+        G += w2 * (g[(1 + NJ) * plane + H] * s - g[(1 + NJ) * plane] * c);
+      } else if (NL == DIM) {
+#pragma unroll
+        for (int k = 0; k < NL; ++k)
+          G += w[k] * w[k] * (g[(1 + NJ + k) * plane + H] * s - g[(1 + NJ + k) * plane] * c);
+      }
+#pragma unroll
+      for (int k = 0; k < DIM; ++k) acc[k] = fmaf(G, w[k], acc[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) {
+      const float v = wave_sum(acc[k]);
+      if (lane == 0) o[k] = v;
+    }
   }
 }
 
@@ -123,15 +221,18 @@ __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) 
 // y (R, M, W), R = 1 + NDIR + NL: GEMM output; plane 0 gets the bias (kept in place as the
 // saved pre-activation).  ACT: h = softplus10(y), J' = σJ, L'_l = σ' Σ_{k∈l} J_k² + σ L_l
 // (σ = σ(10y), σ' = 10σ(1-σ); summed row l covers the J rows k of its endpoint group,
-// l·NDIR/NL <= k < (l+1)·NDIR/NL).  RES: the residual branch (:744, :828) res (R, M, W) is
-// added to every plane first (and the sum kept in y).
+// l·NDIR/NL <= k < (l+1)·NDIR/NL; NL = 0: first derivatives only).  RES: the residual branch
+// (:744, :828) res (R, M, W) is added to every plane first (and the sum kept in y).
 // BIAS = false: y already holds bias + residual (the panel GEMM's epilogue added them,
 // pntf_gemm.hip tt_linear_res); only h is written.
-template <int NDIR, int NL, bool ACT, bool RES, bool BIAS = true>
+// QUIRK (NL = 0): encoder[0] of NN.out_backgrad, whose derivative row is multiplied by
+// σ(10·softplus(y)) instead of σ(10y) (models/model_res_sigmoid_multi.py:435-438).
+template <int NDIR, int NL, bool ACT, bool RES, bool BIAS = true, bool QUIRK = false>
 __global__ __launch_bounds__(256) void tt_act_fwd_kernel(float* __restrict__ y, float* __restrict__ h,
                                   const float* __restrict__ bias, const float* __restrict__ res,
                                   int64_t M, int W) {
-  constexpr int GK = NL ? NDIR / NL : 0;
+  static_assert(!QUIRK || NL == 0, "the out_backgrad quirk is first order");
+  constexpr int GK = NL ? NDIR / (NL ? NL : 1) : 0;
   const int64_t plane = M * W;
   for (int64_t i = 4 * (blockIdx.x * (int64_t)blockDim.x + threadIdx.x); i < plane;
        i += 4 * (int64_t)gridDim.x * blockDim.x) {
@@ -150,6 +251,23 @@ __global__ __launch_bounds__(256) void tt_act_fwd_kernel(float* __restrict__ y, 
       hv[c] = softplus10(v[c]);
     }
     st4(h + i, hv);
+    if (NL == 0) {
+      f4 sJ = s;
+      if (QUIRK) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sJ[c] = sig10(hv[c]);
+      }
+#pragma unroll
+      for (int k = 0; k < NDIR; ++k) {
+        const int64_t iJ = (1 + k) * plane + i;
+        f4 J = ld4(y + iJ);
+        if (RES) {
+          J += ld4(res + iJ);
+          st4(y + iJ, J);
+        }
+        st4(h + iJ, J * sJ);
+      }
+    }
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
       f4 jj = {0.f, 0.f, 0.f, 0.f};
@@ -195,12 +313,15 @@ __device__ __forceinline__ void block_colsum(f4 acc, float* __restrict__ partial
 // Adjoint of act_laplace, in place on g (dL/dh planes in, dL/dy planes out):
 //   g_y = g_h σ + Σ_k g_Jk J_k σ' + Σ_l g_Ll (σ'' Σ_{k∈l} J_k² + L_l σ')   σ'' = 10 σ' (1 - 2σ)
 //   g_Jk = g_Jk σ + 2 g_L(k) J_k σ'      g_Ll = g_Ll σ
-// ACT=false (a Linear with no activation) only forms the bias partials.
-template <int NDIR, int NL, int W, bool ACT>
+// ACT=false (a Linear with no activation) only forms the bias partials.  QUIRK: the adjoint of
+// tt_act_fwd_kernel's out_backgrad encoder[0] (J' = σq J, σq = σ(10 softplus(y)),
+// dσq/dy = 10 σq (1 - σq) σ).
+template <int NDIR, int NL, int W, bool ACT, bool QUIRK = false>
 __global__ __launch_bounds__(256) void tt_act_bwd_kernel(const float* __restrict__ y,
                                                          float* __restrict__ g, int64_t M,
                                                          float* __restrict__ partial) {
-  constexpr int TPR = W / 4, RB = 256 / TPR, GK = NL ? NDIR / NL : 0;
+  static_assert(!QUIRK || NL == 0, "the out_backgrad quirk is first order");
+  constexpr int TPR = W / 4, RB = 256 / TPR, GK = NL ? NDIR / (NL ? NL : 1) : 0;
   const int64_t plane = M * W;
   const int j = 4 * (threadIdx.x % TPR);
   f4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -219,6 +340,24 @@ __global__ __launch_bounds__(256) void tt_act_bwd_kernel(const float* __restrict
       dds[c] = SCALE * ds[c] * (1.f - 2.f * s[c]);
     }
     f4 gy = ld4(g + i) * s;
+    if (NL == 0) {
+      f4 sJ = s, dJ = ds;
+      if (QUIRK) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float q = sig10(softplus10(v[c]));
+          sJ[c] = q;
+          dJ[c] = SCALE * q * (1.f - q) * s[c];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NDIR; ++k) {
+        const int64_t iJ = (1 + k) * plane + i;
+        const f4 J = ld4(y + iJ), gJ = ld4(g + iJ);
+        gy += gJ * J * dJ;
+        st4(g + iJ, gJ * sJ);
+      }
+    }
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
       const int64_t iL = (1 + NDIR + l) * plane + i;
@@ -280,12 +419,17 @@ void launch_reduce(const float* partial, int nb, int W, float* out, int accumula
 }
 
 // ---------------------------------------------------------------- start/goal merge (:761-811)
-// z (2 + DIM, 2n, 128) encoder output planes [value | ∂ (DIM) | Σ∂²] -> u (3 + 2 DIM, n, 256)
-// generator planes [value | ∂xs (DIM) | ∂xg (DIM) | Σ∂²xs | Σ∂²xg], features
-// [max-part | min-part]; c = 10 s0 s1 is the merge curvature (:768-813).
-template <int DIM>
+// z (1 + DIM + NLE, 2n, 128) encoder output planes [value | ∂ (DIM) | NLE second-derivative
+// rows] -> u (1 + 2 DIM + 2 NLE, n, 256) generator planes [value | ∂xs (DIM) | ∂xg (DIM) |
+// L_s (NLE) | L_g (NLE)], features [max-part | min-part]; c = 10 s0 s1 is the merge curvature
+// (:768-813).  NLE = 1: the per-endpoint sums Σ∂²; NLE = DIM: one row per direction; NLE = 0:
+// first derivatives only (out_grad :338-358).  Row l of an endpoint covers its ∂ rows
+// l·DIM/NLE .. (l+1)·DIM/NLE - 1.
+template <int DIM, int NLE>
 __global__ __launch_bounds__(256) void tt_merge_fwd_kernel(const float* __restrict__ z, int64_t n,
                                     float* __restrict__ u) {
+  static_assert(NLE == 0 || NLE == 1 || NLE == DIM, "merge planes");
+  constexpr int GK = NLE ? DIM / (NLE ? NLE : 1) : 0;
   const int64_t pz = 2 * n * H, pu = n * 256;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * H;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -297,7 +441,6 @@ __global__ __launch_bounds__(256) void tt_merge_fwd_kernel(const float* __restri
     u[o] = fmaxf(zs, zg) + lse;
     u[o + H] = fminf(zs, zg) - lse;
     const float s0 = sig10(d), s1 = 1.f - s0, c = SCALE * s0 * s1;
-    float jjs = 0.f, jjg = 0.f;
 #pragma unroll
     for (int k = 0; k < DIM; ++k) {
       const float Js = z[(1 + k) * pz + is], Jg = z[(1 + k) * pz + ig];
@@ -305,22 +448,31 @@ __global__ __launch_bounds__(256) void tt_merge_fwd_kernel(const float* __restri
       u[(1 + k) * pu + o + H] = Js * s1;
       u[(1 + DIM + k) * pu + o] = Jg * s1;
       u[(1 + DIM + k) * pu + o + H] = Jg * s0;
-      jjs = fmaf(Js, Js, jjs);
-      jjg = fmaf(Jg, Jg, jjg);
     }
-    const float Ls = z[(1 + DIM) * pz + is], Lg = z[(1 + DIM) * pz + ig];
-    const float cs = c * jjs, cg = c * jjg;
-    u[(1 + 2 * DIM) * pu + o] = cs + Ls * s0;
-    u[(1 + 2 * DIM) * pu + o + H] = -cs + Ls * s1;
-    u[(2 + 2 * DIM) * pu + o] = cg + Lg * s1;
-    u[(2 + 2 * DIM) * pu + o + H] = -cg + Lg * s0;
+#pragma unroll
+    for (int l = 0; l < NLE; ++l) {
+      float jjs = 0.f, jjg = 0.f;
+#pragma unroll
+      for (int k = l * GK; k < (l + 1) * GK; ++k) {
+        const float Js = z[(1 + k) * pz + is], Jg = z[(1 + k) * pz + ig];
+        jjs = fmaf(Js, Js, jjs);
+        jjg = fmaf(Jg, Jg, jjg);
+      }
+      const float Ls = z[(1 + DIM + l) * pz + is], Lg = z[(1 + DIM + l) * pz + ig];
+      const float cs = c * jjs, cg = c * jjg;
+      u[(1 + 2 * DIM + l) * pu + o] = cs + Ls * s0;
+      u[(1 + 2 * DIM + l) * pu + o + H] = -cs + Ls * s1;
+      u[(1 + 2 * DIM + NLE + l) * pu + o] = cg + Lg * s1;
+      u[(1 + 2 * DIM + NLE + l) * pu + o + H] = -cg + Lg * s0;
+    }
   }
 }
 
-// Adjoint of the merge: gu (3 + 2 DIM, n, 256) -> gz (2 + DIM, 2n, 128).
-template <int DIM>
+// Adjoint of the merge: gu (1 + 2 DIM + 2 NLE, n, 256) -> gz (1 + DIM + NLE, 2n, 128).
+template <int DIM, int NLE>
 __global__ __launch_bounds__(256) void tt_merge_bwd_kernel(const float* __restrict__ z, const float* __restrict__ gu,
                                     int64_t n, float* __restrict__ gz) {
+  constexpr int GK = NLE ? DIM / (NLE ? NLE : 1) : 1, NA = NLE ? NLE : 1;
   const int64_t pz = 2 * n * H, pu = n * 256;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * H;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -329,25 +481,40 @@ __global__ __launch_bounds__(256) void tt_merge_bwd_kernel(const float* __restri
     const int64_t is = p * H + j, ig = (n + p) * H + j, o = p * 256 + j;
     const float d = z[is] - z[ig];
     const float s0 = sig10(d), s1 = 1.f - s0, c = SCALE * s0 * s1;
-    const float Ls = z[(1 + DIM) * pz + is], Lg = z[(1 + DIM) * pz + ig];
-    const float gLsM = gu[(1 + 2 * DIM) * pu + o], gLsm = gu[(1 + 2 * DIM) * pu + o + H];
-    const float gLgM = gu[(2 + 2 * DIM) * pu + o], gLgm = gu[(2 + 2 * DIM) * pu + o + H];
-    const float dLs = gLsM - gLsm, dLg = gLgM - gLgm;
-    float g_s0 = dLs * Ls - dLg * Lg, jjs = 0.f, jjg = 0.f;
+    float dLs[NA], dLg[NA], jjs[NA], jjg[NA], g_s0 = 0.f;
+#pragma unroll
+    for (int l = 0; l < NLE; ++l) {
+      const float Ls = z[(1 + DIM + l) * pz + is], Lg = z[(1 + DIM + l) * pz + ig];
+      const float gLsM = gu[(1 + 2 * DIM + l) * pu + o], gLsm = gu[(1 + 2 * DIM + l) * pu + o + H];
+      const float gLgM = gu[(1 + 2 * DIM + NLE + l) * pu + o];
+      const float gLgm = gu[(1 + 2 * DIM + NLE + l) * pu + o + H];
+      dLs[l] = gLsM - gLsm;
+      dLg[l] = gLgM - gLgm;
+      g_s0 += dLs[l] * Ls - dLg[l] * Lg;
+      jjs[l] = jjg[l] = 0.f;
+      gz[(1 + DIM + l) * pz + is] = gLsM * s0 + gLsm * s1;
+      gz[(1 + DIM + l) * pz + ig] = gLgM * s1 + gLgm * s0;
+    }
 #pragma unroll
     for (int k = 0; k < DIM; ++k) {
       const float Js = z[(1 + k) * pz + is], Jg = z[(1 + k) * pz + ig];
       const float gJsM = gu[(1 + k) * pu + o], gJsm = gu[(1 + k) * pu + o + H];
       const float gJgM = gu[(1 + DIM + k) * pu + o], gJgm = gu[(1 + DIM + k) * pu + o + H];
       g_s0 += (gJsM - gJsm) * Js - (gJgM - gJgm) * Jg;
-      jjs = fmaf(Js, Js, jjs);
-      jjg = fmaf(Jg, Jg, jjg);
-      gz[(1 + k) * pz + is] = gJsM * s0 + gJsm * s1 + 2.f * c * Js * dLs;
-      gz[(1 + k) * pz + ig] = gJgM * s1 + gJgm * s0 + 2.f * c * Jg * dLg;
+      float gs = gJsM * s0 + gJsm * s1, gg = gJgM * s1 + gJgm * s0;
+      if (NLE) {
+        const int l = k / GK;
+        jjs[l] = fmaf(Js, Js, jjs[l]);
+        jjg[l] = fmaf(Jg, Jg, jjg[l]);
+        gs += 2.f * c * Js * dLs[l];
+        gg += 2.f * c * Jg * dLg[l];
+      }
+      gz[(1 + k) * pz + is] = gs;
+      gz[(1 + k) * pz + ig] = gg;
     }
-    gz[(1 + DIM) * pz + is] = gLsM * s0 + gLsm * s1;
-    gz[(1 + DIM) * pz + ig] = gLgM * s1 + gLgm * s0;
-    const float g_c = dLs * jjs + dLg * jjg;
+    float g_c = 0.f;
+#pragma unroll
+    for (int l = 0; l < NLE; ++l) g_c += dLs[l] * jjs[l] + dLg[l] * jjg[l];
     const float kk = (g_s0 + g_c * SCALE * (1.f - 2.f * s0)) * c;
     const float gM = gu[o], gm = gu[o + H];
     gz[is] = gM * s0 + gm * s1 + kk;
@@ -546,6 +713,97 @@ __global__ __launch_bounds__(256) void tt_head_loss_kernel(
   }
 }
 
+// generator[4] + actout_laplace (:693-708) with a GENERAL upstream gradient: the backward of
+// Σ_p (gtau_p τ_p + gdtau_p·∇τ_p + glap_p·Δ_p) for a loss a user writes on NN.out_laplace /
+// out_grad / out_backgrad / Model.gradient outputs.  One wave per pair.  v (R, n, 128),
+// R = 1 + 2 DIM + 2 NLE planes [value | ∂xs | ∂xg | L (2 NLE)]; row l of the second
+// derivatives covers ∂ rows l·GK .. (l+1)·GK - 1, GK = DIM / NLE, so Δ_l = Σ_{k∈l} J_k² τ'' +
+// L_l τ' is the per-direction ∇²τ (NLE = DIM) or the per-endpoint Laplacian (NLE = 1).
+// Outputs (each optional): tau (n), dtau (n, 2 DIM), lap (n, 2 NLE); gv (R, n, 128) = dL/dv
+// and per-block partials of g_w4, g_b4 as tt_head_loss_kernel.  A NULL upstream is zero.
+template <int DIM, int NLE>
+__global__ __launch_bounds__(256) void tt_head_vjp_kernel(
+    const float* __restrict__ v, const float* __restrict__ w4, const float* __restrict__ b4,
+    int64_t n, const float* __restrict__ gtau, const float* __restrict__ gdtau,
+    const float* __restrict__ glap, float* __restrict__ tau, float* __restrict__ dtau,
+    float* __restrict__ lap, float* __restrict__ gv, float* __restrict__ partial) {
+  constexpr int ND = 2 * DIM, NLT = 2 * NLE, R = 1 + ND + NLT, GK = NLE ? DIM / (NLE ? NLE : 1) : 1;
+  constexpr int NA = NLT ? NLT : 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t plane = n * H;
+  const float wa = w4[lane], wb = w4[lane + 64], bias = b4[0];
+  float gwa = 0.f, gwb = 0.f, gb = 0.f;
+  for (int64_t p = blockIdx.x * 4 + wave; p < n; p += (int64_t)gridDim.x * 4) {
+    float yr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float* row = v + r * plane + p * H;
+      yr[r] = wave_sum(fmaf(row[lane], wa, row[lane + 64] * wb));
+    }
+    const float y = yr[0] + bias;
+    const float t = 1.f / (1.f + expf(-0.1f * y));
+    const float dt = 0.1f * t * (1.f - t), ddt = 0.1f * dt * (1.f - 2.f * t);
+    const float dddt = 0.1f * (ddt * (1.f - 2.f * t) - 2.f * dt * dt);
+    if (lane == 0) {
+      if (tau) tau[p] = t;
+      if (dtau) {
+#pragma unroll
+        for (int k = 0; k < ND; ++k) dtau[p * ND + k] = yr[1 + k] * dt;
+      }
+      if (lap) {
+#pragma unroll
+        for (int l = 0; l < NLT; ++l) {
+          float jj = 0.f;
+#pragma unroll
+          for (int k = l * GK; k < (l + 1) * GK; ++k) jj = fmaf(yr[1 + k], yr[1 + k], jj);
+          lap[p * NLT + l] = fmaf(jj, ddt, yr[1 + ND + l] * dt);
+        }
+      }
+    }
+    const float gt = gtau ? gtau[p] : 0.f;
+    float gd[ND], gl[NA];
+#pragma unroll
+    for (int k = 0; k < ND; ++k) gd[k] = gdtau ? gdtau[p * ND + k] : 0.f;
+#pragma unroll
+    for (int l = 0; l < NA; ++l) gl[l] = (NLT && glap) ? glap[p * NLT + l] : 0.f;
+    // actout_laplace adjoint -> g_r of generator[4]'s output rows
+    float g0 = gt * dt;
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      const float J = yr[1 + k];
+      g0 += gd[k] * J * ddt;
+      if (NLT) g0 += gl[k / GK] * J * J * dddt;
+    }
+#pragma unroll
+    for (int l = 0; l < NLT; ++l) g0 += gl[l] * yr[1 + ND + l] * ddt;
+    gb += g0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float g;
+      if (r == 0) g = g0;
+      else if (r <= ND) g = gd[r - 1] * dt + (NLT ? 2.f * gl[(r - 1) / GK] * yr[r] * ddt : 0.f);
+      else g = gl[r - 1 - ND] * dt;
+      const float* row = v + r * plane + p * H;
+      float* grow = gv + r * plane + p * H;
+      gwa = fmaf(g, row[lane], gwa);
+      gwb = fmaf(g, row[lane + 64], gwb);
+      grow[lane] = g * wa;
+      grow[lane + 64] = g * wb;
+    }
+  }
+  __shared__ float red[4][129];
+  red[wave][lane] = gwa;
+  red[wave][lane + 64] = gwb;
+  if (lane == 0) red[wave][128] = gb;
+  __syncthreads();
+  if (threadIdx.x < 129) {
+    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                    red[3][threadIdx.x];
+    if (threadIdx.x < 128) partial[blockIdx.x * 128 + threadIdx.x] = s;
+    else partial[(int64_t)gridDim.x * 128 + blockIdx.x] = s;
+  }
+}
+
 // ---------------------------------------------------------------- AdamW (torch.optim.AdamW)
 // Same operation order as torch's single-tensor AdamW: p *= 1 - lr·wd; m = lerp(m, g, 1-β1);
 // v = β2 v + (1-β2) g²; p -= step_size · m / (sqrt(v)/sqrt(bc2) + eps).
@@ -605,6 +863,40 @@ int nb_for(int64_t rows) {
   return (int)(nb > NB_MAX ? NB_MAX : nb);
 }
 
+// (ndir, nl) of the encoder's Fourier planes: (0, 0), (dim, 0), (dim, 1) or (dim, dim)
+bool fourier_planes_ok(int dim, int ndir, int nl) {
+  return (dim == 3 || dim == 6) &&
+         ((ndir == 0 && nl == 0) || (ndir == dim && (nl == 0 || nl == 1 || nl == dim)));
+}
+
+template <class F>
+void with_fourier(int dim, int ndir, int nl, F&& f) {
+  if (dim == 3) {
+    if (ndir == 0) f(IC<3>{}, IC<0>{}, IC<0>{});
+    else if (nl == 0) f(IC<3>{}, IC<3>{}, IC<0>{});
+    else if (nl == 1) f(IC<3>{}, IC<3>{}, IC<1>{});
+    else f(IC<3>{}, IC<3>{}, IC<3>{});
+  } else {
+    if (ndir == 0) f(IC<6>{}, IC<0>{}, IC<0>{});
+    else if (nl == 0) f(IC<6>{}, IC<6>{}, IC<0>{});
+    else if (nl == 1) f(IC<6>{}, IC<6>{}, IC<1>{});
+    else f(IC<6>{}, IC<6>{}, IC<6>{});
+  }
+}
+
+template <class F>
+void with_merge(int dim, int nle, F&& f) {
+  if (dim == 3) {
+    if (nle == 0) f(IC<3>{}, IC<0>{});
+    else if (nle == 1) f(IC<3>{}, IC<1>{});
+    else f(IC<3>{}, IC<3>{});
+  } else {
+    if (nle == 0) f(IC<6>{}, IC<0>{});
+    else if (nle == 1) f(IC<6>{}, IC<1>{});
+    else f(IC<6>{}, IC<6>{});
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -613,47 +905,66 @@ size_t pntf_tt_partial_floats(void) { return (size_t)NB_MAX * 257; }
 
 const char* pntf_tt_last_error(void) { return g_err; }
 
-int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, const int32_t* env,
-                    int32_t n_env, float* phi, hipStream_t stream) {
-  if ((dim != 3 && dim != 6) || n < 0 || n_env < 1 || (n > 0 && (!xp || !Btab || !phi)))
-    return fail("pntf_tt_fourier: bad arguments");
+int pntf_tt_fourier_ex(int dim, int ndir, int nl, const float* xp, int64_t n, const float* Btab,
+                       const int32_t* env, int32_t n_env, float* phi, hipStream_t stream) {
+  if (!fourier_planes_ok(dim, ndir, nl) || n < 0 || n_env < 1 ||
+      (n > 0 && (!xp || !Btab || !phi)))
+    return fail("pntf_tt_fourier_ex: bad arguments");
   if (n == 0) return PNTF_OK;
   const unsigned g = grid_1d(2 * n * H);
-  if (dim == 3)
-    hipLaunchKernelGGL((tt_fourier_kernel<3>), dim3(g), dim3(256), 0, stream, xp, n, Btab, env,
-                       n_env, phi);
-  else
-    hipLaunchKernelGGL((tt_fourier_kernel<6>), dim3(g), dim3(256), 0, stream, xp, n, Btab, env,
-                       n_env, phi);
+  with_fourier(dim, ndir, nl, [&](auto D, auto NJ, auto NL) {
+    hipLaunchKernelGGL((tt_fourier_kernel<decltype(D)::value, decltype(NJ)::value, decltype(NL)::value>), dim3(g), dim3(256), 0,
+                       stream, xp, n, Btab, env, n_env, phi);
+  });
   return check_launch("tt_fourier_kernel");
+}
+
+int pntf_tt_fourier(int dim, const float* xp, int64_t n, const float* Btab, const int32_t* env,
+                    int32_t n_env, float* phi, hipStream_t stream) {
+  return pntf_tt_fourier_ex(dim, dim, 1, xp, n, Btab, env, n_env, phi, stream);
+}
+
+int pntf_tt_fourier_bwd(int dim, int ndir, int nl, const float* gphi, const float* xp, int64_t n,
+                        const float* Btab, const int32_t* env, int32_t n_env, float* gx,
+                        hipStream_t stream) {
+  if (!fourier_planes_ok(dim, ndir, nl) || n < 0 || n_env < 1 ||
+      (n > 0 && (!gphi || !xp || !Btab || !gx)))
+    return fail("pntf_tt_fourier_bwd: bad arguments");
+  if (n == 0) return PNTF_OK;
+  const unsigned g = grid_1d(2 * n * 64, 4096);   // one wave per point, 4 per workgroup
+  with_fourier(dim, ndir, nl, [&](auto D, auto NJ, auto NL) {
+    hipLaunchKernelGGL((tt_fourier_bwd_kernel<decltype(D)::value, decltype(NJ)::value, decltype(NL)::value>), dim3(g), dim3(256),
+                       0, stream, gphi, xp, n, Btab, env, n_env, gx);
+  });
+  return check_launch("tt_fourier_bwd_kernel");
+}
+
+// every (ndir, nl) of with_planes (hidden: pntf_gemm.hip's pntf_tt_linear_act checks with it)
+extern "C" __attribute__((visibility("hidden"))) int pntf_tt_planes_ok(int ndir, int nl) {
+  return with_planes(ndir, nl, [](auto, auto) {}) ? 1 : 0;
 }
 
 int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, const float* res,
                     int64_t m, int w, int act, hipStream_t stream) {
-  const bool shape = (nl == 0 && ndir == 0) || (nl == 1 && (ndir == 3 || ndir == 6)) ||
-                     (nl == 2 && (ndir == 6 || ndir == 12));
-  if (!shape || m < 0 || (w != 128 && w != 256) || (m > 0 && (!y || !bias || (act && !h))) ||
-      (res && !act))
+  // act: 0 none, 1 softplus10 act_laplace, 2 the out_backgrad encoder[0] quirk (first order)
+  const bool quirk = act == 2;
+  if (!pntf_tt_planes_ok(ndir, nl) || act < 0 || act > 2 ||
+      (quirk && (nl != 0 || (ndir != 3 && ndir != 6))) || m < 0 || (w != 128 && w != 256) ||
+      (m > 0 && (!y || !bias || (act && !h))) || (res && !act))
     return fail("pntf_tt_act_fwd: bad arguments");
   if (m == 0) return PNTF_OK;
   const dim3 g(grid_1d(m * w / 4)), b(256);
-#define PNTF_ACT_FWD(N, L)                                                                  \
-  if (res) hipLaunchKernelGGL((tt_act_fwd_kernel<N, L, true, true>), g, b, 0, stream, y, h,   \
-                              bias, res, m, w);                                             \
-  else if (act) hipLaunchKernelGGL((tt_act_fwd_kernel<N, L, true, false>), g, b, 0, stream, y, \
-                                   h, bias, res, m, w);                                     \
-  else hipLaunchKernelGGL((tt_act_fwd_kernel<N, L, false, false>), g, b, 0, stream, y, h, bias, \
-                          res, m, w);
-  if (nl == 0) {
-    PNTF_ACT_FWD(0, 0)
-  } else if (nl == 1) {
-    if (ndir == 3) { PNTF_ACT_FWD(3, 1) }
-    else { PNTF_ACT_FWD(6, 1) }
-  } else {
-    if (ndir == 6) { PNTF_ACT_FWD(6, 2) }
-    else { PNTF_ACT_FWD(12, 2) }
+  if (quirk) {
+    if (ndir == 3) hipLaunchKernelGGL((tt_act_fwd_kernel<3, 0, true, false, true, true>), g, b, 0, stream, y, h, bias, res, m, w);
+    else hipLaunchKernelGGL((tt_act_fwd_kernel<6, 0, true, false, true, true>), g, b, 0, stream, y, h, bias, res, m, w);
+    return check_launch("tt_act_fwd_kernel<quirk>");
   }
-#undef PNTF_ACT_FWD
+  with_planes(ndir, nl, [&](auto N, auto L) {
+    constexpr int ND = decltype(N)::value, NL = decltype(L)::value;
+    if (res) hipLaunchKernelGGL((tt_act_fwd_kernel<ND, NL, true, true>), g, b, 0, stream, y, h, bias, res, m, w);
+    else if (act) hipLaunchKernelGGL((tt_act_fwd_kernel<ND, NL, true, false>), g, b, 0, stream, y, h, bias, res, m, w);
+    else hipLaunchKernelGGL((tt_act_fwd_kernel<ND, NL, false, false>), g, b, 0, stream, y, h, bias, res, m, w);
+  });
   return check_launch("tt_act_fwd_kernel");
 }
 
@@ -661,89 +972,84 @@ int pntf_tt_act_fwd(int ndir, int nl, float* y, float* h, const float* bias, con
 // reads y, writes h.  Library-internal (not in include/pntf.h).
 extern "C" __attribute__((visibility("hidden"))) int pntf_tt_act_fwd_biased(
     int ndir, int nl, const float* y, float* h, int64_t m, int w, hipStream_t stream) {
-  const bool shape = (nl == 1 && (ndir == 3 || ndir == 6)) || (nl == 2 && (ndir == 6 || ndir == 12));
-  if (!shape || m < 0 || (w != 128 && w != 256) || (m > 0 && (!y || !h)))
+  if (!pntf_tt_planes_ok(ndir, nl) || m < 0 || (w != 128 && w != 256) || (m > 0 && (!y || !h)))
     return fail("pntf_tt_act_fwd_biased: bad arguments");
   if (m == 0) return PNTF_OK;
   const dim3 g(grid_1d(m * w / 4)), b(256);
   float* yy = const_cast<float*>(y);
-  if (nl == 1) {
-    if (ndir == 3) hipLaunchKernelGGL((tt_act_fwd_kernel<3, 1, true, false, false>), g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
-    else hipLaunchKernelGGL((tt_act_fwd_kernel<6, 1, true, false, false>), g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
-  } else {
-    if (ndir == 6) hipLaunchKernelGGL((tt_act_fwd_kernel<6, 2, true, false, false>), g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
-    else hipLaunchKernelGGL((tt_act_fwd_kernel<12, 2, true, false, false>), g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
-  }
+  with_planes(ndir, nl, [&](auto N, auto L) {
+    hipLaunchKernelGGL((tt_act_fwd_kernel<decltype(N)::value, decltype(L)::value, true, false, false>),
+                       g, b, 0, stream, yy, h, nullptr, nullptr, m, w);
+  });
   return check_launch("tt_act_fwd_kernel<biased>");
 }
 
 int pntf_tt_act_bwd(int ndir, int nl, const float* y, float* g, int64_t m, int w, int act,
                     float* gbias, int accumulate, float* partial, hipStream_t stream) {
-  const bool shape = (nl == 0 && ndir == 0) || (nl == 1 && (ndir == 3 || ndir == 6)) ||
-                     (nl == 2 && (ndir == 6 || ndir == 12));
-  if (!shape || m < 0 || (w != 128 && w != 256) || !gbias || !partial ||
-      (m > 0 && (!g || (act && !y))))
+  const bool quirk = act == 2;
+  if (!pntf_tt_planes_ok(ndir, nl) || act < 0 || act > 2 ||
+      (quirk && (nl != 0 || (ndir != 3 && ndir != 6) || w != 128)) || m < 0 ||
+      (w != 128 && w != 256) || !gbias || !partial || (m > 0 && (!g || (act && !y))))
     return fail("pntf_tt_act_bwd: bad arguments");
   const int nb = nb_for(m / (1024 / w));
   const dim3 gr(nb), b(256);
-#define PNTF_ACT_BWD(N, L, W)                                                              \
-  if (act) hipLaunchKernelGGL((tt_act_bwd_kernel<N, L, W, true>), gr, b, 0, stream, y, g, m,  \
-                              partial);                                                     \
-  else hipLaunchKernelGGL((tt_act_bwd_kernel<N, L, W, false>), gr, b, 0, stream, y, g, m, \
-                          partial);
-  if (nl == 0) {   // value plane only (the first-order tape)
-    if (w == 128) { PNTF_ACT_BWD(0, 0, 128) }
-    else { PNTF_ACT_BWD(0, 0, 256) }
-  } else if (nl == 1) {   // encoder planes are 128 wide
-    if (w != 128) return fail("pntf_tt_act_bwd: encoder planes are 128 wide");
-    if (ndir == 3) { PNTF_ACT_BWD(3, 1, 128) }
-    else { PNTF_ACT_BWD(6, 1, 128) }
-  } else if (w == 128) {
-    if (ndir == 6) { PNTF_ACT_BWD(6, 2, 128) }
-    else { PNTF_ACT_BWD(12, 2, 128) }
+  if (quirk) {
+    if (ndir == 3) hipLaunchKernelGGL((tt_act_bwd_kernel<3, 0, 128, true, true>), gr, b, 0, stream, y, g, m, partial);
+    else hipLaunchKernelGGL((tt_act_bwd_kernel<6, 0, 128, true, true>), gr, b, 0, stream, y, g, m, partial);
   } else {
-    if (ndir == 6) { PNTF_ACT_BWD(6, 2, 256) }
-    else { PNTF_ACT_BWD(12, 2, 256) }
+    with_planes(ndir, nl, [&](auto N, auto L) {
+      constexpr int ND = decltype(N)::value, NL = decltype(L)::value;
+      if (w == 128) {
+        if (act) hipLaunchKernelGGL((tt_act_bwd_kernel<ND, NL, 128, true>), gr, b, 0, stream, y, g, m, partial);
+        else hipLaunchKernelGGL((tt_act_bwd_kernel<ND, NL, 128, false>), gr, b, 0, stream, y, g, m, partial);
+      } else {
+        if (act) hipLaunchKernelGGL((tt_act_bwd_kernel<ND, NL, 256, true>), gr, b, 0, stream, y, g, m, partial);
+        else hipLaunchKernelGGL((tt_act_bwd_kernel<ND, NL, 256, false>), gr, b, 0, stream, y, g, m, partial);
+      }
+    });
   }
-#undef PNTF_ACT_BWD
   launch_reduce(partial, nb, w, gbias, accumulate, stream);
   return check_launch("tt_act_bwd_kernel");
 }
 
-int pntf_tt_merge_fwd(int dim, const float* z, int64_t n, float* u, hipStream_t stream) {
-  if ((dim != 3 && dim != 6) || n < 0 || (n > 0 && (!z || !u)))
+int pntf_tt_merge_fwd_ex(int dim, int nle, const float* z, int64_t n, float* u,
+                         hipStream_t stream) {
+  if ((dim != 3 && dim != 6) || (nle != 0 && nle != 1 && nle != dim) || n < 0 ||
+      (n > 0 && (!z || !u)))
     return fail("pntf_tt_merge_fwd: bad arguments");
   if (n == 0) return PNTF_OK;
   const dim3 g(grid_1d(n * H)), b(256);
-  if (dim == 3) hipLaunchKernelGGL((tt_merge_fwd_kernel<3>), g, b, 0, stream, z, n, u);
-  else hipLaunchKernelGGL((tt_merge_fwd_kernel<6>), g, b, 0, stream, z, n, u);
+  with_merge(dim, nle, [&](auto D, auto L) {
+    hipLaunchKernelGGL((tt_merge_fwd_kernel<decltype(D)::value, decltype(L)::value>), g, b, 0, stream, z, n, u);
+  });
   return check_launch("tt_merge_fwd_kernel");
+}
+
+int pntf_tt_merge_bwd_ex(int dim, int nle, const float* z, const float* gu, int64_t n, float* gz,
+                         hipStream_t stream) {
+  if ((dim != 3 && dim != 6) || (nle != 0 && nle != 1 && nle != dim) || n < 0 ||
+      (n > 0 && (!z || !gu || !gz)))
+    return fail("pntf_tt_merge_bwd: bad arguments");
+  if (n == 0) return PNTF_OK;
+  const dim3 g(grid_1d(n * H)), b(256);
+  with_merge(dim, nle, [&](auto D, auto L) {
+    hipLaunchKernelGGL((tt_merge_bwd_kernel<decltype(D)::value, decltype(L)::value>), g, b, 0, stream, z, gu, n, gz);
+  });
+  return check_launch("tt_merge_bwd_kernel");
+}
+
+int pntf_tt_merge_fwd(int dim, const float* z, int64_t n, float* u, hipStream_t stream) {
+  return pntf_tt_merge_fwd_ex(dim, 1, z, n, u, stream);
 }
 
 int pntf_tt_merge_bwd(int dim, const float* z, const float* gu, int64_t n, float* gz,
                       hipStream_t stream) {
-  if ((dim != 3 && dim != 6) || n < 0 || (n > 0 && (!z || !gu || !gz)))
-    return fail("pntf_tt_merge_bwd: bad arguments");
-  if (n == 0) return PNTF_OK;
-  const dim3 g(grid_1d(n * H)), b(256);
-  if (dim == 3) hipLaunchKernelGGL((tt_merge_bwd_kernel<3>), g, b, 0, stream, z, gu, n, gz);
-  else hipLaunchKernelGGL((tt_merge_bwd_kernel<6>), g, b, 0, stream, z, gu, n, gz);
-  return check_launch("tt_merge_bwd_kernel");
+  return pntf_tt_merge_bwd_ex(dim, 1, z, gu, n, gz, stream);
 }
 
 int pntf_tt_fourier_value(int dim, const float* xp, int64_t n, const float* Btab,
                           const int32_t* env, int32_t n_env, float* phi, hipStream_t stream) {
-  if ((dim != 3 && dim != 6) || n < 0 || n_env < 1 || (n > 0 && (!xp || !Btab || !phi)))
-    return fail("pntf_tt_fourier_value: bad arguments");
-  if (n == 0) return PNTF_OK;
-  const unsigned g = grid_1d(2 * n * H);
-  if (dim == 3)
-    hipLaunchKernelGGL((tt_fourier_kernel<3, false>), dim3(g), dim3(256), 0, stream, xp, n, Btab,
-                       env, n_env, phi);
-  else
-    hipLaunchKernelGGL((tt_fourier_kernel<6, false>), dim3(g), dim3(256), 0, stream, xp, n, Btab,
-                       env, n_env, phi);
-  return check_launch("tt_fourier_kernel<value>");
+  return pntf_tt_fourier_ex(dim, 0, 0, xp, n, Btab, env, n_env, phi, stream);
 }
 
 int pntf_tt_merge_value_fwd(const float* z, int64_t n, float* u, hipStream_t stream) {
@@ -808,6 +1114,29 @@ int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const f
   launch_reduce(partial, nb, 128, gw4, 0, stream);
   launch_reduce(partial + (int64_t)nb * 128, nb, 1, gb4, 0, stream);
   return check_launch("tt_head_loss_kernel");
+}
+
+int pntf_tt_head_vjp(int dim, int nle, const float* v, const float* w4, const float* b4,
+                     int64_t n, const float* gtau, const float* gdtau, const float* glap,
+                     float* tau, float* dtau, float* lap, float* gv, float* gw4, float* gb4,
+                     float* partial, hipStream_t stream) {
+  if ((dim != 3 && dim != 6) || (nle != 0 && nle != 1 && nle != dim) || n < 0 || !w4 || !b4 ||
+      !gw4 || !gb4 || !partial || (glap && nle == 0) || (lap && nle == 0) ||
+      (n > 0 && (!v || !gv)))
+    return fail("pntf_tt_head_vjp: bad arguments");
+  if (n == 0) {
+    hipMemsetAsync(gw4, 0, 128 * sizeof(float), stream);
+    hipMemsetAsync(gb4, 0, sizeof(float), stream);
+    return check_launch("pntf_tt_head_vjp");
+  }
+  const int nb = nb_for((n + 3) / 4);
+  with_merge(dim, nle, [&](auto D, auto L) {
+    hipLaunchKernelGGL((tt_head_vjp_kernel<decltype(D)::value, decltype(L)::value>), dim3(nb), dim3(256), 0, stream, v,
+                       w4, b4, n, gtau, gdtau, glap, tau, dtau, lap, gv, partial);
+  });
+  launch_reduce(partial, nb, 128, gw4, 0, stream);
+  launch_reduce(partial + (int64_t)nb * 128, nb, 1, gb4, 0, stream);
+  return check_launch("tt_head_vjp_kernel");
 }
 
 int pntf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,

@@ -12,7 +12,7 @@ import torch
 
 from pntf import ops
 from pntf import train as _train
-from pntf.net import PackedCache, TauFunction, build_layers, weight_term
+from pntf.net import PackedCache, build_layers, guard_epilogue, out_tau, taylor_outputs
 from pntf.net import init_weights as _init_weights
 
 from .model_res_sigmoid_multi import (DDSigmoid_out, DSigmoid, DSigmoid_out, Sigmoid,  # noqa
@@ -85,22 +85,28 @@ class NN(torch.nn.Module):
 
     def out(self, coords):
         coords = coords.clone().detach().requires_grad_(True)
-        Bt = self._B(coords.device)
-        tau = TauFunction.apply(coords, Bt, None, self.packed(), self.dim)
-        wt = weight_term(self, coords, Bt, None, self.dim)   # reference: autograd to the weights
-        return (tau if wt is None else tau + wt), coords
+        return out_tau(self, coords, self._B(coords.device), None, self.dim), coords
 
     def out_grad(self, coords):
-        t, d = ops.tau_grad(self.packed(), coords, self._B(coords.device), None, self.dim,
-                            ops.GRAD_EXACT)
+        """(τ (N,1), ∇τ (N,2dim), coords) (:513-613); differentiable w.r.t. coords and every
+        weight when autograd records."""
+        t, d = taylor_outputs(self, coords, self._B(coords.device), None, self.dim, 1, False)
+        return t.unsqueeze(1), d, coords
+
+    def out_backgrad(self, coords):
+        """:300-511.  Unlike the multi model's, the arm's out_backgrad carries the exact
+        forward-mode ∇τ (its derivative rows use σ(10y) at every layer, :330-333); the shape
+        probes it prints (:502-507) are not repeated."""
+        t, d = taylor_outputs(self, coords, self._B(coords.device), None, self.dim, 1, False)
         return t.unsqueeze(1), d, coords
 
     def out_laplace(self, coords):
         """Taylor mode (models/model_res_sigmoid.py:676-826): coords (N, 2dim) ->
-        (τ (N,1), ∇τ (N,2dim), diagonal ∇²τ (N,2dim), coords)."""
-        out = ops.eikonal_residual(self.packed(), coords, self._B(coords.device), None,
-                                   self.dim, want=("tau", "dtau", "ltau"))
-        return out["tau"].unsqueeze(1), out["dtau"], out["ltau"], coords
+        (τ (N,1), ∇τ (N,2dim), diagonal ∇²τ (N,2dim), coords), coords a fresh grad leaf (:678)
+        that receives the gradient of a loss on the outputs (as do the weights)."""
+        coords = coords.clone().detach().requires_grad_(True)
+        t, d, l = taylor_outputs(self, coords, self._B(coords.device), None, self.dim, 2, False)
+        return t.unsqueeze(1), d, l, coords
 
     def forward(self, coords):
         coords = coords.clone().detach().requires_grad_(True)
@@ -272,24 +278,41 @@ class Model:
 
     def TravelTimes(self, Xp):
         Xp = Xp.to(self._dev())
-        return ops.travel_time(self.network.packed(), Xp, self.network._B(Xp.device), None,
-                               self.dim)
+        out = ops.travel_time(self.network.packed(), Xp, self.network._B(Xp.device), None,
+                              self.dim)
+        return guard_epilogue(self.network, out, "Model.TravelTimes")
 
     def Tau(self, Xp):
         Xp = Xp.to(self._dev())
-        return ops.tau(self.network.packed(), Xp, self.network._B(Xp.device), None,
-                       self.dim).unsqueeze(1)
+        out = ops.tau(self.network.packed(), Xp, self.network._B(Xp.device), None,
+                      self.dim).unsqueeze(1)
+        return guard_epilogue(self.network, out, "Model.Tau")
 
     def Speed(self, Xp):
         Xp = Xp.to(self._dev())
-        return ops.speed(self.network.packed(), Xp, self.network._B(Xp.device), None, self.dim)
+        out = ops.speed(self.network.packed(), Xp, self.network._B(Xp.device), None, self.dim)
+        return guard_epilogue(self.network, out, "Model.Speed")
+
+    def Speed2(self, Xp, gamma):
+        """Speed at the goal with the viscosity term (:1218-1245): 1 / (sqrt(S)/τ² + γ Δ_gτ)
+        from out_laplace's τ, ∇τ and the goal's Laplacian Σ_d ∂²τ/∂x_goal_d²."""
+        Xp = Xp.to(self._dev())
+        tau, dtau, ltau, _ = self.network.out_laplace(Xp)
+        d = self.dim
+        lap1 = ltau[:, d:].sum(-1)
+        D = Xp[:, d:] - Xp[:, :d]
+        T0 = (D * D).sum(1)
+        DT1 = dtau[:, d:]
+        t = tau[:, 0]
+        S = T0 * (DT1 * DT1).sum(1) - 2 * t * (DT1 * D).sum(1) + t * t
+        return 1 / (torch.sqrt(S) / (t * t) + gamma * lap1)
 
     def Gradient(self, Xp):
         """Path velocity from the exact ∇τ (autograd in the reference, :1247-1282)."""
         Xp = Xp.to(self._dev())
         v, _ = ops.path_velocity(self.network.packed(), Xp, self.network._B(Xp.device), None,
                                  self.dim, ops.GRAD_EXACT)
-        return v
+        return guard_epilogue(self.network, v, "Model.Gradient")
 
     def Plan(self, XP, step=0.015, tol=0.03, max_iter=300):
         """Batched test/arm_plan.py:140-152 loop on device (exact ∇τ, per-query freeze)."""

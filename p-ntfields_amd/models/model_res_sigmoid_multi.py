@@ -29,7 +29,7 @@ import torch
 
 from pntf import ops
 from pntf import train as _train
-from pntf.net import PackedCache, TauFunction, build_layers, weight_term
+from pntf.net import PackedCache, build_layers, guard_epilogue, out_tau, taylor_outputs
 from pntf.net import init_weights as _init_weights
 
 
@@ -111,36 +111,34 @@ class NN(torch.nn.Module):
 
     def out(self, coords, B, env=None):
         """τ (N,1) and the fresh grad-leaf coords (:215-259).  `env` (N,) int picks rows of a
-        per-env B table (E,dim,128); the reference passes a single (dim,128) B."""
+        per-env B table (E,dim,128); the reference passes a single (dim,128) B.  τ is
+        differentiable w.r.t. coords (the fused reverse sweep; ∇τ itself differentiable under
+        create_graph) and every weight (the HIP value tape), as the reference's graph is."""
         coords = coords.clone().detach().requires_grad_(True)
-        Bt = _as_table(B, coords.device)
-        tau = TauFunction.apply(coords, Bt, env, self.packed(), self.dim)
-        wt = weight_term(self, coords, Bt, env, self.dim)   # reference: autograd to the weights
-        return (tau if wt is None else tau + wt), coords
+        return out_tau(self, coords, _as_table(B, coords.device), env, self.dim), coords
 
     def out_grad(self, coords, B, env=None):
         """(τ (N,1), ∇τ (N,2dim), coords) — forward-mode Jacobian in the reference (:303-400);
-        the same values come from the exact HIP reverse sweep."""
-        t, d = ops.tau_grad(self.packed(), coords, _as_table(B, coords.device), env, self.dim,
-                            ops.GRAD_EXACT)
+        the same values come from the exact HIP reverse sweep.  Differentiable w.r.t. coords
+        and every weight (first-order Taylor tape) when autograd records."""
+        t, d = taylor_outputs(self, coords, _as_table(B, coords.device), env, self.dim, 1, False)
         return t.unsqueeze(1), d, coords
 
     def out_backgrad(self, coords, B, env=None):
         """(τ, dτ, coords) of the reference's manual reverse mode (:402-647), including its
-        encoder[0] derivative quirk (:435-438) that test/gib_plan.py plans with."""
-        t, d = ops.tau_grad(self.packed(), coords, _as_table(B, coords.device), env, self.dim,
-                            ops.GRAD_BACKGRAD_COMPAT)
+        encoder[0] derivative quirk (:435-438) that test/gib_plan.py plans with; differentiable
+        like out_grad (the tape carries the quirk)."""
+        t, d = taylor_outputs(self, coords, _as_table(B, coords.device), env, self.dim, 1, True)
         return t.unsqueeze(1), d, coords
 
     def out_laplace(self, coords, B):
         """Taylor mode (:710-848): coords (E, n, 2dim), B (E, dim, 128) per env ->
-        (τ (E,n,1), ∇τ (E,n,2dim), diagonal ∇²τ (E,n,2dim), coords)."""
+        (τ (E,n,1), ∇τ (E,n,2dim), diagonal ∇²τ (E,n,2dim), coords).  Differentiable w.r.t.
+        coords and every weight (the HIP Taylor tape with the incoming gradients)."""
         E, n, _ = coords.shape
-        out = ops.eikonal_residual(self.packed(), coords.reshape(E * n, -1),
-                                   _as_table(B, coords.device), _env_ids(E, n, coords.device),
-                                   self.dim, want=("tau", "dtau", "ltau"))
-        return (out["tau"].view(E, n, 1), out["dtau"].view(E, n, -1),
-                out["ltau"].view(E, n, -1), coords)
+        t, d, l = taylor_outputs(self, coords.reshape(E * n, -1), _as_table(B, coords.device),
+                                 _env_ids(E, n, coords.device), self.dim, 2, False)
+        return t.view(E, n, 1), d.view(E, n, -1), l.view(E, n, -1), coords
 
     def forward(self, coords, B, env=None):
         coords = coords.clone().detach().requires_grad_(True)
@@ -191,8 +189,8 @@ class Model:
             loss_n = total + reg
             return beta * loss_n, loss_n, diff.view(E, n)
         out = ops.eikonal_residual(self.network.packed(), points.reshape(E * n, -1), Bt,
-                                   _env_ids(E, n, dev), self.dim,
-                                   yobs=Yobs.reshape(E * n, 2), gamma=gamma, want=("diff",))
+                                  _env_ids(E, n, dev), self.dim,
+                                  yobs=Yobs.reshape(E * n, 2), gamma=gamma, want=("diff",))
         diff = out["diff"].view(E, n)
         loss_n = (ops.device_sum(diff) / E / n).float() + reg
         return beta * loss_n, loss_n, diff
@@ -326,20 +324,23 @@ class Model:
     def TravelTimes(self, Xp):
         """|x_g - x_s| / τ (:1173-1186), uses self.B."""
         Xp = Xp.to(self._dev())
-        return ops.travel_time(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
-                               self.dim)
+        out = ops.travel_time(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                              self.dim)
+        return guard_epilogue(self.network, out, "Model.TravelTimes")
 
     def Tau(self, Xp):
         """τ (N,1) (:1188-1193), uses self.B."""
         Xp = Xp.to(self._dev())
-        return ops.tau(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
-                       self.dim).unsqueeze(1)
+        out = ops.tau(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                      self.dim).unsqueeze(1)
+        return guard_epilogue(self.network, out, "Model.Tau")
 
     def Speed(self, Xp):
         """Speed at the goal (:1195-1216), uses self.B."""
         Xp = Xp.to(self._dev())
-        return ops.speed(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
-                         self.dim)
+        out = ops.speed(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                        self.dim)
+        return guard_epilogue(self.network, out, "Model.Speed")
 
     def Gradient(self, Xp, B, env=None):
         """Path velocity [v_s | v_g] (:1218-1248) from the out_backgrad sweep (quirk kept),
@@ -347,7 +348,7 @@ class Model:
         Xp = Xp.to(self._dev())
         v, _ = ops.path_velocity(self.network.packed(), Xp, _as_table(B, Xp.device), env,
                                  self.dim, ops.GRAD_BACKGRAD_COMPAT)
-        return v
+        return guard_epilogue(self.network, v, "Model.Gradient")
 
     def Plan(self, XP, B, step=0.03, tol=0.06, max_iter=500, env=None,
              mode=ops.GRAD_BACKGRAD_COMPAT):

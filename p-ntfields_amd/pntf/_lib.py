@@ -83,6 +83,21 @@ SIGNATURES = {
                                          _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32,
                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                          _c_void_p]),
+    # general VJP tape (out_laplace / out_grad / out_backgrad / Model.gradient backward)
+    "pntf_tt_fourier_ex": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_void_p,
+                                          _i64, _c_void_p, _c_void_p, _i32, _c_void_p,
+                                          _c_void_p]),
+    "pntf_tt_fourier_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_void_p,
+                                           _c_void_p, _i64, _c_void_p, _c_void_p, _i32,
+                                           _c_void_p, _c_void_p]),
+    "pntf_tt_merge_fwd_ex": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _i64,
+                                            _c_void_p, _c_void_p]),
+    "pntf_tt_merge_bwd_ex": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _c_void_p,
+                                            _i64, _c_void_p, _c_void_p]),
+    "pntf_tt_head_vjp": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _c_void_p,
+                                        _c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p,
+                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                        _c_void_p, _c_void_p, _c_void_p]),
     "pntf_tt_gemm_work_floats": (ctypes.c_size_t, [_i64, _i64, _i64]),
     "pntf_tt_gemm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _c_void_p, _i64,
                                     _c_void_p, _i64, _c_void_p, _i64, _f32, _c_void_p,

@@ -102,22 +102,29 @@ def gemm(C, A, B, ta, tb, beta=0.0):
 
 class _Tape:
     """Forward tape of one loss evaluation: (name, input planes, pre-activation planes, act,
-    has_residual) per Linear, in execution order."""
+    has_residual) per Linear, in execution order.  `nle` second-derivative rows per endpoint:
+    1 (the per-endpoint sums of the Eikonal loss), dim (one per direction: a general loss on
+    out_laplace's ∇²τ) or 0 (first derivatives only: a loss on ∇τ).  `fused` allows the fused
+    input-gradient kernel (pntf_tt_linear_bwd), which takes the Loss / value layouts only."""
 
-    def __init__(self, params, dim, device):
+    def __init__(self, params, dim, device, nle=1, fused=True):
         self.p = params
         self.dim = dim
         self.dev = device
         self.s = _stream(device)
         self.lib = _lib.load()
         self.ops = []
+        self.nle = nle
+        self.fused = fused
 
     def planes(self, R):
-        """(ndir, nl) of a Taylor tensor with R planes: (dim, 1) in the encoder, (2dim, 2)
+        """(ndir, nl) of a Taylor tensor with R planes: (dim, nle) in the encoder, (2dim, 2nle)
         after the merge (pntf_train.hip); (0, 0) for the value-only tape of NN.out."""
         if R == 1:
             return (0, 0)
-        return (self.dim, 1) if R == 2 + self.dim else (2 * self.dim, 2)
+        if R == 1 + self.dim + self.nle:
+            return (self.dim, self.nle)
+        return (2 * self.dim, 2 * self.nle)
 
     def lin(self, x3, name, act=True, res=None):
         W, b = self.p[name + ".weight"], self.p[name + ".bias"]
@@ -130,13 +137,14 @@ class _Tape:
         # GEMM and the act kernel where the fused one would not balance)
         work = _work(self.dev, int(self.lib.pntf_tt_gemm_work_floats(R * M, N, K)))
         st = self.lib.pntf_tt_linear_act(ndir, nl, _vp(x3), M, K, _vp(W), N, _vp(b), _vp(res),
-                                         _vp(y), _vp(h), int(act), _LINEAR_ACT, _vp(work),
+                                         _vp(y), _vp(h), int(act),
+                                         _LINEAR_ACT if self.fused else 2, _vp(work),
                                          work.numel(), self.s)
         if st != 0:
             raise PntfError("pntf_tt_linear_act: %s | %s" % (
                 self.lib.pntf_tt_gemm_last_error().decode(),
                 self.lib.pntf_tt_last_error().decode()))
-        self.ops.append((name, x3, y, act, res is not None))
+        self.ops.append((name, x3, y, int(act), res is not None))
         return h if act else y
 
 
@@ -194,12 +202,13 @@ def loss_grad(params, xp, yobs, Btab, env, dim, gamma, scale, arm, grads):
     return diff
 
 
-def _adjoint(tape, g, grads, part, merge_bwd):
+def _adjoint(tape, g, grads, part, merge_bwd, want_input=False):
     """Walk the tape back from g = dL/d(generator[3] output planes): per Linear the act adjoint
     (+ bias gradient), the weight gradient and the input gradient; merge_bwd(g) at the merge.
     With _LINEAR_BWD the input gradient of a Linear and the act adjoint of the layer before it
     run as one kernel (pntf_tt_linear_bwd) wherever that layer's output feeds this one directly
-    (not across the merge)."""
+    (not across the merge).  want_input: returns dL/dΦ, the Fourier planes' gradient (one more
+    GEMM through encoder[0]); otherwise None."""
     lib, s, dev, params = tape.lib, tape.s, tape.dev, tape.p
     pending = []
     order = list(reversed(tape.ops))
@@ -215,13 +224,18 @@ def _adjoint(tape, g, grads, part, merge_bwd):
         g2 = g.view(R * M, N)
         weight_grad(g2, x3.view(R * M, K), grads[name + ".weight"])
         if name == "encoder.0":
-            break
+            if not want_input:
+                return None
+            gphi = torch.empty((R, M, K), dtype=torch.float32, device=dev)
+            gemm(gphi.view(R * M, K), g2, params[name + ".weight"], ta=False, tb=False)
+            return gphi
         if has_res:
             pending.append(g)
         W = params[name + ".weight"]
         prev = order[idx + 1]
         res = pending.pop() if name in _BLOCK_HEADS else None
-        use_bwd = (M >= _BWD_FUSED_MIN_POINTS) if _LINEAR_BWD is None else bool(_LINEAR_BWD)
+        use_bwd = tape.fused and ((M >= _BWD_FUSED_MIN_POINTS) if _LINEAR_BWD is None
+                                  else bool(_LINEAR_BWD))
         fused_in = use_bwd and name != "generator.0" and prev[3]
         if fused_in:
             # gx = act_bwd_prev(g·W (+ res)): in place into the residual branch's buffer
@@ -292,6 +306,74 @@ def tau_weight_grad(params, xp, Btab, env, dim, gtau, grads):
         return gz
     _adjoint(tape, g, grads, part, merge_bwd)
     return tau
+
+
+def field_vjp(params, xp, Btab, env, dim, nle, quirk, gtau, gdtau, glap, grads, want_x):
+    """The backward of Σ_p (gtau_p·τ_p + gdtau_p·∇τ_p + glap_p·Δ_p) through the Taylor graph of
+    NN.out_laplace (models/model_res_sigmoid_multi.py:710-848), NN.out_grad (:303-400),
+    NN.out_backgrad (quirk: encoder[0]'s derivative row scaled by σ(10·softplus(y)),
+    :435-438) or Model.gradient's ∇τ (:890-896): what the reference's autograd leaves in
+    every trained parameter's `.grad` (written into `grads`, key -> tensor shaped like the
+    parameter) and, with want_x, returns as coords' gradient (n, 2dim).
+
+    nle second-derivative rows per endpoint: 0 (a loss on τ and ∇τ only), 1 (glap (n, 2) on
+    each endpoint's Laplacian Σ_d ∂²τ/∂x_d², the rows the Eikonal loss uses) or dim (glap
+    (n, 2dim) on the diagonal ∇²τ).  gtau (n,), gdtau (n, 2dim), glap: device tensors or None
+    (zero).  Tape: the Fourier planes (pntf_tt_fourier_ex), per Linear one GEMM + the fused
+    bias/residual/act kernel, the merge (pntf_tt_merge_fwd_ex), generator[4] + actout_laplace
+    with the upstream gradient (pntf_tt_head_vjp), the adjoint sweep of the training step, and
+    the Fourier adjoint for the coordinates (pntf_tt_fourier_bwd).  Returns gx or None."""
+    dev = xp.device
+    lib = _lib.load()
+    n = xp.shape[0]
+    if nle not in (0, 1, dim) or (quirk and nle):
+        raise PntfError("field_vjp: nle must be 0, 1 or dim (0 with the out_backgrad quirk)")
+    if n == 0:
+        for g in grads.values():
+            g.zero_()
+        return torch.empty((0, 2 * dim), dtype=torch.float32, device=dev) if want_x else None
+    tape = _Tape(params, dim, dev, nle=nle, fused=False)
+    s = tape.s
+    Re, Rg = 1 + dim + nle, 1 + 2 * dim + 2 * nle
+    n_env = Btab.shape[0]
+    phi = torch.empty((Re, 2 * n, 2 * H), dtype=torch.float32, device=dev)
+    check(lib.pntf_tt_fourier_ex(dim, dim, nle, _vp(xp), n, _vp(Btab), _vp(env), n_env, _vp(phi),
+                                 s), "pntf_tt_fourier_ex")
+    h = tape.lin(phi, "encoder.0", act=2 if quirk else 1)
+    for i in (1, 2):
+        a = tape.lin(h, "encoder.%d" % i)
+        h = tape.lin(a, "encoder1.%d" % i, res=h)
+    z = tape.lin(h, "encoder.3", act=False)
+    u = torch.empty((Rg, n, 2 * H), dtype=torch.float32, device=dev)
+    check(lib.pntf_tt_merge_fwd_ex(dim, nle, _vp(z), n, _vp(u), s), "pntf_tt_merge_fwd_ex")
+    for i in (0, 1, 2):
+        a = tape.lin(u, "generator.%d" % i)
+        u = tape.lin(a, "generator1.%d" % i, res=u)
+    v = tape.lin(u, "generator.3")
+    g = torch.empty_like(v)
+    part = _partial(dev)
+
+    def dev32(t):
+        return None if t is None else t.detach().to(device=dev, dtype=torch.float32).contiguous()
+    gtau, gdtau, glap = dev32(gtau), dev32(gdtau), dev32(glap)
+    check(lib.pntf_tt_head_vjp(dim, nle, _vp(v), _vp(params["generator.4.weight"]),
+                               _vp(params["generator.4.bias"]), n, _vp(gtau), _vp(gdtau),
+                               _vp(glap), None, None, None, _vp(g),
+                               _vp(grads["generator.4.weight"]), _vp(grads["generator.4.bias"]),
+                               _vp(part), s), "pntf_tt_head_vjp")
+
+    def merge_bwd(gu):
+        gz = torch.empty((Re, 2 * n, H), dtype=torch.float32, device=dev)
+        check(lib.pntf_tt_merge_bwd_ex(dim, nle, _vp(z), _vp(gu), n, _vp(gz), s),
+              "pntf_tt_merge_bwd_ex")
+        return gz
+    gphi = _adjoint(tape, g, grads, part, merge_bwd, want_input=want_x)
+    if not want_x:
+        return None
+    gx = torch.empty((n, 2 * dim), dtype=torch.float32, device=dev)
+    check(lib.pntf_tt_fourier_bwd(dim, dim, nle, _vp(gphi), _vp(xp), n, _vp(Btab), _vp(env),
+                                  n_env, _vp(gx), s), "pntf_tt_fourier_bwd")
+    return gx
 
 
 def module_params(module):

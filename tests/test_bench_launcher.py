@@ -30,7 +30,7 @@ def _line(r):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("gpus", [2, 4])
+@pytest.mark.parametrize("gpus", [2, 4, 8])
 def test_launcher_weak_scaling(gpus):
     j = _line(_run(["--gpus", str(gpus), "--rehearse", "--steps", "3", "--warmup", "1",
                     "--pairs", "1000"]))
@@ -40,11 +40,16 @@ def test_launcher_weak_scaling(gpus):
     assert j["gather_ok"] and j["steps"] == 3
 
 
-def test_launcher_strong_scaling_uneven():
-    j = _line(_run(["--gpus", "3", "--rehearse", "--steps", "2", "--warmup", "0",
-                    "--total-pairs", "1001"]))
-    assert j["scaling"] == "strong" and j["global_batch"] == 1001
-    assert j["pairs_per_rank0"] == 334 and j["gather_ok"]
+@pytest.mark.parametrize("gpus,total,rank0", [(3, 1001, 334), (8, 1027, 129),
+                                              (8, 1 << 23, 1 << 20)])
+def test_launcher_strong_scaling_uneven(gpus, total, rank0):
+    """--total-pairs split over the ranks, including the deployment size of 8 (the C4 8M
+    workload, 8 x 1M pairs, and an uneven 1027)."""
+    j = _line(_run(["--gpus", str(gpus), "--rehearse", "--steps", "2", "--warmup", "0",
+                    "--total-pairs", str(total)]))
+    assert j["scaling"] == "strong" and j["global_batch"] == total
+    assert j["n_gpus"] == gpus and j["world_size"] == gpus
+    assert j["pairs_per_rank0"] == rank0 and j["gather_ok"]
 
 
 def test_single_rank_rehearsal():

@@ -82,3 +82,45 @@ def test_gloo_world1_forced_collective():
     test_rccl.py::test_rccl_world1_allgather drives over RCCL)."""
     mp.start_processes(_worker_ws1, args=(_free_port(),), nprocs=1, join=True,
                        start_method="spawn")
+
+
+def _worker_c5(rank, world, port, q, max_iter):
+    """One rank of the sharded C5 exchange (bench.py shard_gather_plans) with the fp32 oracle
+    planner standing in for the HIP kernel; rank 0 checks the gathered paths and step counts
+    against the unsharded plan, query by query."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as tdist
+    import bench
+    from oracle import pntf_oracle as O
+    from pntf import synth
+    torch.set_num_threads(1)
+    dist.init("gloo")
+    W = synth.make_weights(0)
+    Ba = synth.make_B(6, seed=12, arm=True).T
+    xq = synth.make_box_pairs(q, 6, seed=3)
+
+    def plan_local(x):
+        p, s = O.plan(W, x, Ba, dim=6, step=0.015, tol=0.03, max_iter=max_iter, compat=False,
+                      dtype=np.float32)
+        return torch.from_numpy(p.astype(np.float32)), torch.from_numpy(s.astype(np.int32))
+    paths, steps = bench.shard_gather_plans(plan_local, xq, rank, world)
+    assert paths.shape == (q, max_iter + 2, 12) and steps.shape == (q,)
+    if rank == 0:
+        pf, sf = plan_local(xq)
+        assert torch.equal(steps, sf)
+        # each shard is planned alone, so only the fp32 summation order of the batch differs
+        assert float((paths - pf).abs().max()) < 1e-5
+        assert torch.equal(paths[:, 0], torch.from_numpy(xq))        # query order kept
+    tdist.barrier()
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("q", [1024, 1027])
+def test_gloo_world8_c5_sharded_gather(q):
+    """The deployment size: 8 ranks, the C5 1024 queries (128 per rank) and an uneven 1027
+    (129 on ranks 0-2, 128 on the rest), gathered in query order (bench.py
+    sharded_extras).  4 planner steps keep the oracle's CPU time small."""
+    port = _free_port()
+    mp.start_processes(_worker_c5, args=(8, port, q, 4), nprocs=8, join=True,
+                       start_method="spawn")

@@ -118,3 +118,210 @@ def test_oracle_vjp_value_only_is_tau_weight_grad():
     assert rel_l2(dx, dx0) < 1e-12
     for k in g0:
         assert rel_l2(g[k], g0[k]) < 1e-12, k
+
+
+# ------------------------------------------------------------------------------ GPU
+def _drop_in(tag, dim, dev, f):
+    """The drop-in net and Model at the fixture's weights, and the method calls the golden
+    script made on the reference (make_out_grad_goldens.py record_vjp)."""
+    W = {k: torch.from_numpy(v) for k, v in _weights(tag, dim).items()}
+    if dim == 3:
+        from models import model_res_sigmoid_multi as md
+        net = md.NN(dev, 3)
+        model = md.Model(".", ".", 3, 2, device=dev)
+        Bt = torch.from_numpy(f["Btab"]).to(dev)
+        B0 = Bt[0]
+        calls = {"laplace": lambda x: net.out_laplace(x, Bt),
+                 "grad": lambda x: net.out_grad(x, B0),
+                 "backgrad": lambda x: net.out_backgrad(x, B0),
+                 "out": lambda x: net.out(x, B0)}
+    else:
+        from models import model_res_sigmoid as ma
+        net = ma.NN(dev, 6, torch.from_numpy(f["B"]))
+        model = ma.Model(".", ".", 6, device=dev)
+        calls = {"laplace": lambda x: net.out_laplace(x), "grad": lambda x: net.out_grad(x),
+                 "backgrad": lambda x: net.out_backgrad(x), "out": lambda x: net.out(x)}
+    net.load_state_dict(W, strict=True)
+    net.to(dev)
+    model.network = net
+    return net, model, calls
+
+
+def run_method(net, model, calls, f, meth, dim, dev):
+    """The fixture's loss for `meth` through the drop-in, backward; returns (tau, dtau, ltau,
+    dcoords) as numpy."""
+    xp = torch.from_numpy(f["xp"]).to(dev)
+    n = xp.shape[0]
+    E = int(f["E"])
+    wt = torch.from_numpy(f["w/wt"]).to(dev)
+    wd = torch.from_numpy(f["w/wd"]).to(dev)
+    net.zero_grad(set_to_none=True)
+    x = xp.clone().requires_grad_(True)
+    lt = None
+    if meth.startswith("laplace"):
+        wl = (torch.from_numpy(f["w/wl"]) if meth == "laplace"
+              else torch.from_numpy(np.repeat(f["w/wl_sum"], dim, axis=1))).to(dev)
+        tau, dtau, ltau, X = calls["laplace"](x.view(E, n // E, 2 * dim) if E else x)
+        tau, dtau, ltau = tau.reshape(n), dtau.reshape(n, 2 * dim), ltau.reshape(n, 2 * dim)
+        loss = (wt * tau).sum() + (wd * dtau).sum() + (wl * ltau).sum()
+        leaf = X if X.is_leaf else x
+        lt = ltau.detach().cpu().numpy()
+    elif meth == "gradient2":
+        tau, leaf = calls["out"](xp)
+        dtau = model.gradient(tau, leaf)
+        tau = tau.reshape(n)
+        loss = (wt * tau).sum() + (wd * dtau).sum()
+    else:
+        tau, dtau, _ = calls[meth](x)
+        tau = tau.reshape(n)
+        loss = (wt * tau).sum() + (wd * dtau).sum()
+        leaf = x
+    loss.backward()
+    dc = leaf.grad.cpu().numpy() if leaf.grad is not None else None
+    return tau.detach().cpu().numpy(), dtau.detach().cpu().numpy(), lt, dc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag,dim", CASES)
+@pytest.mark.parametrize("meth", METHODS)
+def test_drop_in_vjp_vs_reference(tag, dim, meth):
+    """`.backward()` of a weighted sum of out_laplace / out_grad / out_backgrad / create_graph
+    Model.gradient outputs fills every weight's `.grad` and coords' gradient as the
+    reference's autograd does (fixtures from the reference itself)."""
+    dev = torch.device("cuda:0")
+    f = load("vjp_%s_d%d.npz" % (tag, dim))
+    net, model, calls = _drop_in(tag, dim, dev, f)
+    t, d, lt, dc = run_method(net, model, calls, f, meth, dim, dev)
+    # outputs: per pair against the fp64 oracle at the north star's 1e-4
+    B, env, compat = _oracle_args(f, meth, dim)
+    (to, do, lo), go, dxo = O.taylor_vjp(_weights(tag, dim), f["xp"], B, env, dim,
+                                         *_upstream(f, meth, dim), compat=compat)
+    assert per_pair(t, to) < 1e-4 and per_pair(d, do) < 1e-4, meth
+    if lt is not None:
+        assert per_pair(lt, lo) < 1e-4
+    assert dc is not None, "coords received no gradient"
+    e_dc = float(np.abs(dc - f[meth + "/dcoords"]).max() / np.abs(f[meth + "/dcoords"]).max())
+    assert e_dc < GRAD_TOL, (meth, e_dc)
+    grads = {k: (p.grad.cpu().numpy() if p.grad is not None else None)
+             for k, p in net.named_parameters()}
+    worst = check_grads(f, meth, grads, GRAD_TOL)
+    print("%s %s d%d: coords %.2e, worst param %.2e" % (meth, tag, dim, e_dc, worst))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 37])
+@pytest.mark.parametrize("nle", ["none", "sum", "dir"])
+def test_field_vjp_ragged_env_table_vs_oracle(n, nle):
+    """field_vjp on ragged batches with a per-pair env table (random env ids) against the fp64
+    oracle: all three second-derivative layouts (none / per-endpoint sums / per direction)."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    W = synth.make_weights(0)
+    xp = synth.make_pairs(n, 3, seed=60 + n)
+    Bt = synth.make_B_table(3, 3)
+    env = synth.make_env_ids(n, 3, contiguous=False, seed=n)
+    rng = np.random.Generator(np.random.PCG64(n))
+    gt = rng.uniform(-1, 1, n)
+    gd = rng.uniform(-1, 1, (n, 6))
+    gl = None if nle == "none" else rng.uniform(-1, 1, (n, 6))
+    if nle == "sum":
+        gl = np.repeat(gl[:, [0, 3]], 3, axis=1)
+    _, go, dxo = O.taylor_vjp(W, xp, Bt, env, 3, gt, gd, gl)
+    p = {k: torch.from_numpy(v).to(dev) for k, v in W.items() if not k.startswith("encoder1.0")}
+    grads = {k: torch.empty_like(v) for k, v in p.items()}
+    cuda = lambda a: None if a is None else torch.from_numpy(np.asarray(a, np.float32)).to(dev)  # noqa
+    glap = {"none": None, "sum": cuda(None if gl is None else gl[:, [0, 3]]), "dir": cuda(gl)}[nle]
+    k = {"none": 0, "sum": 1, "dir": 3}[nle]
+    gx = train.field_vjp(p, cuda(xp), cuda(Bt), torch.from_numpy(env).to(dev), 3, k, False,
+                         cuda(gt), cuda(gd), glap, grads, True)
+    assert float(np.abs(gx.cpu().numpy() - dxo).max() / np.abs(dxo).max()) < GRAD_TOL
+    for key, g in grads.items():
+        r = go[key]
+        assert float(np.abs(g.cpu().numpy() - r).max() / np.abs(r).max()) < GRAD_TOL, key
+
+
+@pytest.mark.gpu
+def test_frozen_layers_get_no_grad_and_others_match():
+    """with encoder layers frozen (requires_grad False) a backward through NN.out
+    and through out_laplace works, leaves the frozen parameters without .grad and gives the
+    trainable ones the same gradient as the unfrozen net."""
+    from models import model_res_sigmoid_multi as md
+    dev = torch.device("cuda:0")
+    W = {k: torch.from_numpy(v) for k, v in synth.make_weights(0).items()}
+    xp = torch.from_numpy(synth.make_pairs(50, 3, seed=70)).to(dev)
+    Bt = torch.from_numpy(synth.make_B_table(2, 3)).to(dev)
+
+    def grads(frozen):
+        net = md.NN(dev, 3)
+        net.load_state_dict(W, strict=True)
+        net.to(dev)
+        for name in frozen:
+            getattr(net, name.split(".")[0])[int(name.split(".")[1])].requires_grad_(False)
+        tau, _ = net.out(xp, Bt[0])
+        t2, d2, l2, _ = net.out_laplace(xp.view(2, 25, 6), Bt)
+        (tau.sum() + d2.sum() + l2.pow(2).sum()).backward()
+        return {k: (None if p.grad is None else p.grad.clone()) for k, p in net.named_parameters()}
+
+    ref = grads([])
+    fr = grads(["encoder.0", "encoder.1"])
+    for k, g in fr.items():
+        if k.startswith(("encoder.0.", "encoder.1.", "encoder1.0.")):
+            assert g is None, k
+        else:
+            assert torch.allclose(g, ref[k], rtol=1e-5, atol=1e-7), k
+
+
+@pytest.mark.gpu
+def test_epilogue_outputs_raise_on_backward_and_b_grad_raises():
+    """Model.Speed / Tau / TravelTimes / Gradient are fused epilogue kernels: differentiating
+    them raises instead of silently training nothing; so does asking for B's gradient."""
+    from models import model_res_sigmoid_multi as md
+    from pntf.ops import PntfError
+    dev = torch.device("cuda:0")
+    net = md.NN(dev, 3)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.make_weights(0).items()})
+    net.to(dev)
+    m = md.Model(".", ".", 3, 2, device=dev)
+    m.network = net
+    m.B = torch.from_numpy(synth.make_B(3)).to(dev)
+    xp = torch.from_numpy(synth.make_pairs(8, 3, seed=71)).to(dev)
+    for fn in (m.Speed, m.Tau, m.TravelTimes, lambda x: m.Gradient(x, m.B)):
+        with pytest.raises(PntfError):
+            fn(xp).sum().backward()
+    with torch.no_grad():
+        assert m.Speed(xp).grad_fn is None            # inference: nothing attached
+    B = m.B.clone().requires_grad_(True)
+    t, d, _ = net.out_grad(xp, B)
+    with pytest.raises(PntfError):
+        d.sum().backward()
+
+
+@pytest.mark.gpu
+def test_fused_bwd_multi_round_matches_two_kernel():
+    """the fused input-gradient kernel (pntf_tt_linear_bwd, default for layers of
+    >= 100 000 points) at a size where every workgroup strides over several 32-point blocks
+    (8 192 pairs: 16 384 encoder points = 512 blocks per column group over <= 256
+    workgroups) agrees with the GEMM + act pair on the loss gradients."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    W = synth.make_weights(0)
+    n = 8192
+    p = {k: torch.from_numpy(v).to(dev) for k, v in W.items() if not k.startswith("encoder1.0")}
+    xp = torch.from_numpy(synth.make_pairs(n, 3, seed=72)).to(dev)
+    yobs = torch.from_numpy(synth.make_speeds(n, seed=73)).to(dev)
+    Bt = torch.from_numpy(synth.make_B_table(2, 3)).to(dev)
+    env = torch.from_numpy(synth.make_env_ids(n, 2)).to(dev)
+    out = {}
+    saved = train._LINEAR_BWD
+    try:
+        for mode in (0, 1):
+            train._LINEAR_BWD = mode
+            grads = {k: torch.empty_like(v) for k, v in p.items()}
+            diff = train.loss_grad(p, xp, yobs, Bt, env, 3, 1e-3, 1.0 / n, False, grads)
+            out[mode] = (diff, grads)
+    finally:
+        train._LINEAR_BWD = saved
+    assert torch.allclose(out[0][0], out[1][0])
+    for k in p:
+        a, b = out[0][1][k], out[1][1][k]
+        assert float((a - b).abs().max() / b.abs().max()) < 1e-4, k

@@ -30,7 +30,7 @@ if __name__ == "__main__":
     def c5():
         res["p"] = ops.plan(packed, xq, Ba, dim=6, step=0.015, tol=0.03, max_iter=199,
                             mode=ops.GRAD_EXACT, schedule=sched)
-    ms = bench._timeit(c5, reps=reps)
+    ms = bench._timeit(c5, reps=reps, warm=5)
     st = res["p"][1]
     # active queries per step and the step at which at most one query per CU is left (the
     # tail hand-off point of the AUTO schedule)

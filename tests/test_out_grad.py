@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import GOLDEN, load, rel_l2
+from golden_util import GOLDEN, load, north_star_pairs, rel_l2
 from oracle import pntf_oracle as O
 from pntf import synth
 
@@ -78,6 +78,9 @@ def test_out_weight_grads_vs_reference(tag, dim):
     tau, coords = call(torch.from_numpy(f["xp"]).to(dev))
     (tau[:, 0] * torch.from_numpy(f["wt"]).to(dev)).sum().backward()
     assert np.abs(tau.detach().cpu().numpy()[:, 0] - f["tau"]).max() < 1e-5
+    B = f["B"] if dim == 3 else f["B"].T
+    north_star_pairs("out_grad_%s_d%d tau" % (tag, dim), tau.detach().cpu().numpy()[:, 0],
+                     f["tau"], O.forward(_weights(tag, dim), f["xp"], B, dim=dim)[:, 0])
     assert _rel(coords.grad.cpu().numpy(), f["dcoords"]) < GRAD_TOL
     for k, p in net.named_parameters():
         if k.startswith("encoder1.0."):

@@ -40,7 +40,8 @@ class StreamScratch:
         buf = self.entries.pop(key, None)
         if buf is None or buf.numel() < numel:
             buf = torch.empty(max(int(numel), 1), dtype=self.dtype, device=device)
-            buf.record_stream(stream)
+            if not torch.cuda.is_current_stream_capturing():
+                buf.record_stream(stream)     # (a graph's pool keeps its buffers alive)
         self.entries[key] = buf
         while len(self.entries) > self.cap:
             self.entries.popitem(last=False)

@@ -237,7 +237,10 @@ def test_field_vjp_ragged_env_table_vs_oracle(n, nle):
     assert float(np.abs(gx.cpu().numpy() - dxo).max() / np.abs(dxo).max()) < GRAD_TOL
     for key, g in grads.items():
         r = go[key]
-        assert float(np.abs(g.cpu().numpy() - r).max() / np.abs(r).max()) < GRAD_TOL, key
+        # the head bias gradient is one sum over the pairs of ±-weighted terms and can cancel
+        # to far below its terms: it is held relative to the head weight gradient's scale
+        scale = np.abs(go["generator.4.weight"]).max() if r.size == 1 else np.abs(r).max()
+        assert float(np.abs(g.cpu().numpy() - r).max() / scale) < GRAD_TOL, key
 
 
 @pytest.mark.gpu

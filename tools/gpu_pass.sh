@@ -12,6 +12,9 @@
 #   c5                     C5 planner: kernel trace + stats, then the SQ / TCC / LDS PMC passes
 #   q1                     batch-1 Gibson planner step probe (tools/q1_probe.py)
 #   train                  training-step kernel trace at 2 x 10 000 pairs (tools/prof_train.sh)
+#   py=<tool.py args>      a probe script (tools/*.py), output <tag>_<tool>.txt
+#   trace=<tool.py args>   the same under rocprofv3 --kernel-trace --stats, plus the idle-gap
+#                          summary of tools/trace_gaps.py
 #   smoke                  __graft_entry__.smoke()
 # Outputs land in gpurun_out/<tag>_*; tools/prof_summary.py / c5_pmc_summary.py turn them
 # into profiles/.
@@ -58,6 +61,17 @@ for step in "$@"; do
       bash tools/prof_train.sh > "$OUT/${TAG}_train_prof.txt" 2>&1
       rm -rf "$OUT/${TAG}_prof_train"; mv "$OUT/prof_train" "$OUT/${TAG}_prof_train"
       cat "$OUT/${TAG}_train_prof.txt" ;;
+    py=*)       # py=<tool.py args...>: a probe script, output <tag>_<tool>.txt
+      a=${step#py=}; nm=$(basename ${a%% *} .py)
+      timeout -k 10 600 python3 $a > "$OUT/${TAG}_$nm.txt" 2>&1 || { tail -30 "$OUT/${TAG}_$nm.txt"; exit 1; }
+      tail -5 "$OUT/${TAG}_$nm.txt" ;;
+    trace=*)    # trace=<tool.py args...>: kernel trace (no counters) + idle-gap summary
+      a=${step#trace=}; nm=$(basename ${a%% *} .py)
+      ( cd /tmp && export TMPDIR=/tmp
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_trace_$nm" -o run \
+          --output-format csv -- python3 $R/$a > "$OUT/${TAG}_trace_$nm.log" 2>&1 )
+      f=$(find "$OUT/${TAG}_trace_$nm" -name "*kernel_trace.csv" | head -1)
+      python3 tools/trace_gaps.py "$f" | tee "$OUT/${TAG}_trace_$nm.gaps" ;;
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $step"; exit 2 ;;

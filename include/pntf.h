@@ -78,6 +78,19 @@ size_t pntf_packed_floats(void);
 int pntf_pack_weights(const float* const* params, int n_params, float* packed,
                       hipStream_t stream);
 
+/* Handle form of the same: pntf_net_create allocates the packed weights
+ * (hipMalloc) and packs `params` as pntf_pack_weights does; every entry point below takes
+ * pntf_net_packed(net) as its `packed` argument.  pntf_net_update repacks after a weight
+ * change (Model.load / an optimizer step, models/model_res_sigmoid_multi.py:1154-1166);
+ * pntf_net_destroy frees the buffer (hipFree: call it once the stream's work that reads it
+ * is done).  pntf_net_create returns NULL on error (pntf_last_error). */
+typedef struct pntf_net pntf_net;
+pntf_net* pntf_net_create(const float* const* params, int n_params, hipStream_t stream);
+int pntf_net_update(pntf_net* net, const float* const* params, int n_params,
+                    hipStream_t stream);
+const float* pntf_net_packed(const pntf_net* net);
+void pntf_net_destroy(pntf_net* net);
+
 /* DEFAULT kernel schedule of pntf_tau / _tau_grad / _path_velocity / _speed / _travel_time
  * (PNTF_SCHED_*, see pntf_plan_ex; AUTO unless changed).  Process-wide, so not thread-safe
  * against concurrent calls: callers that need a specific schedule pass it per call through

@@ -4,6 +4,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <new>
+
 #include "pntf.h"
 
 #include "pntf_common.h"
@@ -372,6 +374,43 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
   hipLaunchKernelGGL(pack_quad_aux_kernel, dim3(Q_WAVES * Q_NAUX), dim3(256), 0, stream,
                      packed + OFF_BIAS, packed + OFF_QUAD);
   return check_launch("pack_weights");
+}
+
+// ---- handle form: the library owns the packed weights
+struct pntf_net {
+  float* packed;
+};
+
+pntf_net* pntf_net_create(const float* const* params, int n_params, hipStream_t stream) {
+  float* p = nullptr;
+  if (hipMalloc(&p, sizeof(float) * PACKED_TOTAL) != hipSuccess) {
+    fail(PNTF_ERR_HIP, "pntf_net_create: hipMalloc of the packed weights failed%s");
+    return nullptr;
+  }
+  if (pntf_pack_weights(params, n_params, p, stream) != PNTF_OK) {
+    hipFree(p);
+    return nullptr;
+  }
+  pntf_net* net = new (std::nothrow) pntf_net{p};
+  if (!net) {
+    hipFree(p);
+    fail(PNTF_ERR_ARG, "pntf_net_create: out of host memory%s");
+  }
+  return net;
+}
+
+int pntf_net_update(pntf_net* net, const float* const* params, int n_params,
+                    hipStream_t stream) {
+  if (!net) return fail(PNTF_ERR_ARG, "pntf_net_update: null handle%s");
+  return pntf_pack_weights(params, n_params, net->packed, stream);
+}
+
+const float* pntf_net_packed(const pntf_net* net) { return net ? net->packed : nullptr; }
+
+void pntf_net_destroy(pntf_net* net) {
+  if (!net) return;
+  hipFree(net->packed);
+  delete net;
 }
 
 int pntf_tau(const float* packed, int dim, const float* xp, int64_t n, const float* Btab,

@@ -343,11 +343,12 @@ class Model:
         XP[:, self.dim + 0] = X.ravel()
         XP[:, self.dim + 1] = Y.ravel()
         XP = torch.from_numpy(XP.astype(np.float32)).to(self._dev())
-        tt = self.TravelTimes(XP)
-        ss = self.Speed(XP)
-        tau = self.Tau(XP)
-        return (X, Y, tt.cpu().numpy().reshape(X.shape), ss.cpu().numpy().reshape(X.shape),
-                tau.cpu().numpy().reshape(X.shape))
+        with torch.no_grad():          # plotting values: nothing to differentiate
+            tt = self.TravelTimes(XP)
+            ss = self.Speed(XP)
+            tau = self.Tau(XP)
+            return (X, Y, tt.cpu().numpy().reshape(X.shape), ss.cpu().numpy().reshape(X.shape),
+                    tau.cpu().numpy().reshape(X.shape))
 
     def plot(self, epoch, total_train_loss, alpha):
         """Model.plot (:1284-1329): speed and τ maps with travel-time contours, saved as

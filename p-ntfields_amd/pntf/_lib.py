@@ -27,6 +27,11 @@ SIGNATURES = {
     "pntf_packed_floats": (_size, []),
     "pntf_pack_weights": (ctypes.c_int, [ctypes.POINTER(_c_void_p), ctypes.c_int, _c_void_p,
                                          _c_void_p]),
+    "pntf_net_create": (_c_void_p, [ctypes.POINTER(_c_void_p), ctypes.c_int, _c_void_p]),
+    "pntf_net_update": (ctypes.c_int, [_c_void_p, ctypes.POINTER(_c_void_p), ctypes.c_int,
+                                       _c_void_p]),
+    "pntf_net_packed": (_c_void_p, [_c_void_p]),
+    "pntf_net_destroy": (None, [_c_void_p]),
     "pntf_workspace_bytes": (_size, [_i64]),
     "pntf_field_schedule_for": (ctypes.c_int, [_i64, ctypes.c_int]),
     "pntf_set_field_schedule": (ctypes.c_int, [ctypes.c_int]),

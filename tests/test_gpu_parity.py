@@ -82,52 +82,52 @@ def T(a, dev, dtype=torch.float32):
 def test_tau_grad_exact_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3, mode=ops.GRAD_EXACT, schedule=field_schedule)
-    check(t.cpu().numpy(), "fwd_grad_d3.npz", "tau")
-    check(d.cpu().numpy(), "fwd_grad_d3.npz", "dtau")
-    check(d.cpu().numpy(), "fwd_grad_d3.npz", "dtau_fwdmode")
+    check(t.detach().cpu().numpy(), "fwd_grad_d3.npz", "tau")
+    check(d.detach().cpu().numpy(), "fwd_grad_d3.npz", "dtau")
+    check(d.detach().cpu().numpy(), "fwd_grad_d3.npz", "dtau_fwdmode")
 
 
 def test_tau_only_kernel(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     t = ops.tau(packed, T(f["xp"], dev), T(f["B"], dev), dim=3, schedule=field_schedule)
-    check(t.cpu().numpy(), "fwd_grad_d3.npz", "tau")
+    check(t.detach().cpu().numpy(), "fwd_grad_d3.npz", "tau")
 
 
 def test_backgrad_compat_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     t, d = ops.tau_grad(packed, T(f["xp"], dev), T(f["B"], dev), dim=3,
                         mode=ops.GRAD_BACKGRAD_COMPAT, schedule=field_schedule)
-    check(t.cpu().numpy(), "fwd_grad_d3.npz", "tau_backgrad")
-    check(d.cpu().numpy(), "fwd_grad_d3.npz", "dtau_backgrad")
+    check(t.detach().cpu().numpy(), "fwd_grad_d3.npz", "tau_backgrad")
+    check(d.detach().cpu().numpy(), "fwd_grad_d3.npz", "dtau_backgrad")
 
 
 def test_epilogues_vs_reference(packed, dev, field_schedule):
     f = load("fwd_grad_d3.npz")
     xp, B = T(f["xp"], dev), T(f["B"], dev)
     v, _ = ops.path_velocity(packed, xp, B, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT, schedule=field_schedule)
-    check(v.cpu().numpy(), "fwd_grad_d3.npz", "gradient")
-    check(ops.speed(packed, xp, B, dim=3, schedule=field_schedule).cpu().numpy(), "fwd_grad_d3.npz", "speed")
-    check(ops.travel_time(packed, xp, B, dim=3, schedule=field_schedule).cpu().numpy(), "fwd_grad_d3.npz", "travel_time")
+    check(v.detach().cpu().numpy(), "fwd_grad_d3.npz", "gradient")
+    check(ops.speed(packed, xp, B, dim=3, schedule=field_schedule).detach().cpu().numpy(), "fwd_grad_d3.npz", "speed")
+    check(ops.travel_time(packed, xp, B, dim=3, schedule=field_schedule).detach().cpu().numpy(), "fwd_grad_d3.npz", "travel_time")
 
 
 def test_env_table_vs_reference(packed, dev, field_schedule):
     g = load("fwd_grad_env_d3.npz")
     xp, Bt, env = T(g["xp"], dev), T(g["B_table"], dev), T(g["env"], dev, torch.int32)
     t, d = ops.tau_grad(packed, xp, Bt, env, dim=3, schedule=field_schedule)
-    check(t.cpu().numpy(), "fwd_grad_env_d3.npz", "tau")
-    check(d.cpu().numpy(), "fwd_grad_env_d3.npz", "dtau")
+    check(t.detach().cpu().numpy(), "fwd_grad_env_d3.npz", "tau")
+    check(d.detach().cpu().numpy(), "fwd_grad_env_d3.npz", "dtau")
     _, dc = ops.tau_grad(packed, xp, Bt, env, dim=3, mode=ops.GRAD_BACKGRAD_COMPAT, schedule=field_schedule)
-    check(dc.cpu().numpy(), "fwd_grad_env_d3.npz", "dtau_backgrad")
+    check(dc.detach().cpu().numpy(), "fwd_grad_env_d3.npz", "dtau_backgrad")
 
 
 def test_arm_dim6_vs_reference(packed, dev, field_schedule):
     a = load("fwd_grad_d6.npz")
     xp, B = T(a["xp"], dev), T(a["B"].T, dev)
     t, d = ops.tau_grad(packed, xp, B, dim=6, schedule=field_schedule)
-    check(t.cpu().numpy(), "fwd_grad_d6.npz", "tau")
-    check(d.cpu().numpy(), "fwd_grad_d6.npz", "dtau")
+    check(t.detach().cpu().numpy(), "fwd_grad_d6.npz", "tau")
+    check(d.detach().cpu().numpy(), "fwd_grad_d6.npz", "dtau")
     v, _ = ops.path_velocity(packed, xp[:16], B, dim=6, mode=ops.GRAD_EXACT, schedule=field_schedule)
-    check(v.cpu().numpy(), "fwd_grad_d6.npz", "gradient16")
+    check(v.detach().cpu().numpy(), "fwd_grad_d6.npz", "gradient16")
 
 
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 33, 1000, 4099])
@@ -137,8 +137,8 @@ def test_ragged_batches_vs_oracle(packed, dev, W, field_schedule, n):
     env = synth.make_env_ids(n, 3, contiguous=False, seed=n)
     t, d = ops.tau_grad(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3, schedule=field_schedule)
     to, do = O.tau_grad(W, xp, Bt, env)
-    close(t.cpu().numpy(), to[:, 0], pairs=True)
-    close(d.cpu().numpy(), do, pairs=True)
+    close(t.detach().cpu().numpy(), to[:, 0], pairs=True)
+    close(d.detach().cpu().numpy(), do, pairs=True)
 
 
 def test_empty_batch(packed, dev):
@@ -154,7 +154,7 @@ def test_invalid_env_gives_nan(packed, dev, field_schedule):
     env[3] = 7
     env[11] = -1
     t, d = ops.tau_grad(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3, schedule=field_schedule)
-    t, d = t.cpu().numpy(), d.cpu().numpy()
+    t, d = t.detach().cpu().numpy(), d.detach().cpu().numpy()
     assert np.isnan(t[3]) and np.isnan(t[11]) and np.isnan(d[3]).all()
     ok = np.ones(20, bool)
     ok[[3, 11]] = False
@@ -185,8 +185,8 @@ def test_coincident_endpoints(packed, dev, W):
     B = synth.make_B(3)
     t, d = ops.tau_grad(packed, T(x, dev), T(B, dev), dim=3)
     to, do = O.tau_grad(W, x, B)
-    close(t.cpu().numpy(), to[:, 0], pairs=True)
-    close(d.cpu().numpy(), do, pairs=True)
+    close(t.detach().cpu().numpy(), to[:, 0], pairs=True)
+    close(d.detach().cpu().numpy(), do, pairs=True)
 
 
 @pytest.mark.parametrize("schedule", ["wave_tile", "split_tile", "quad_tile"])
@@ -195,7 +195,7 @@ def test_gibson_planner_vs_reference(packed, dev, schedule):
     path, steps = ops.plan(packed, T(p["starts"], dev), T(p["B"], dev), dim=3, step=0.03,
                            tol=0.06, max_iter=500, mode=ops.GRAD_BACKGRAD_COMPAT,
                            schedule=schedule)
-    path, steps = path.cpu().numpy(), steps.cpu().numpy()
+    path, steps = path.detach().cpu().numpy(), steps.detach().cpu().numpy()
     np.testing.assert_array_equal(steps, p["iters"])
     assert np.abs(path - p["paths"]).max() < 1e-3
     # endpoints
@@ -208,7 +208,7 @@ def test_arm_planner_vs_reference(packed, dev, schedule):
     p = load("plan_arm.npz")
     path, steps = ops.plan(packed, T(p["starts"], dev), T(p["B"].T, dev), dim=6, step=0.015,
                            tol=0.03, max_iter=300, mode=ops.GRAD_EXACT, schedule=schedule)
-    path, steps = path.cpu().numpy(), steps.cpu().numpy()
+    path, steps = path.detach().cpu().numpy(), steps.detach().cpu().numpy()
     np.testing.assert_array_equal(steps, p["iters"])
     assert np.abs(path - p["paths"]).max() < 1e-3
 
@@ -221,8 +221,8 @@ def test_planner_batch_vs_oracle(packed, dev, schedule, W):
     path, steps = ops.plan(packed, T(xp0, dev), T(B, dev), dim=6, step=0.015, tol=0.03,
                            max_iter=60, mode=ops.GRAD_EXACT, schedule=schedule)
     po, so = O.plan(W, xp0, B, dim=6, step=0.015, tol=0.03, max_iter=60, compat=False)
-    np.testing.assert_array_equal(steps.cpu().numpy(), so)
-    assert np.abs(path.cpu().numpy() - po).max() < 1e-3
+    np.testing.assert_array_equal(steps.detach().cpu().numpy(), so)
+    assert np.abs(path.detach().cpu().numpy() - po).max() < 1e-3
 
 
 @pytest.mark.parametrize("dim,compat", [(3, True), (6, False)])
@@ -259,14 +259,14 @@ def test_drop_in_models_api(W, dev):
     assert tau.shape == (1024, 1)
     dtau = m.gradient(tau, coords)
     check(tau.detach().cpu().numpy(), "fwd_grad_d3.npz", "tau")
-    check(dtau.cpu().numpy(), "fwd_grad_d3.npz", "dtau")
-    check(m.Gradient(xp.clone(), B).cpu().numpy(), "fwd_grad_d3.npz", "gradient")
+    check(dtau.detach().cpu().numpy(), "fwd_grad_d3.npz", "dtau")
+    check(m.Gradient(xp.clone(), B).detach().cpu().numpy(), "fwd_grad_d3.npz", "gradient")
     m.B = B
-    check(m.Speed(xp).cpu().numpy(), "fwd_grad_d3.npz", "speed")
-    check(m.TravelTimes(xp).cpu().numpy(), "fwd_grad_d3.npz", "travel_time")
-    check(m.Tau(xp).cpu().numpy(), "fwd_grad_d3.npz", "tau")
+    check(m.Speed(xp).detach().cpu().numpy(), "fwd_grad_d3.npz", "speed")
+    check(m.TravelTimes(xp).detach().cpu().numpy(), "fwd_grad_d3.npz", "travel_time")
+    check(m.Tau(xp).detach().cpu().numpy(), "fwd_grad_d3.npz", "tau")
     t2, d2, _ = m.network.out_backgrad(xp, B)
-    check(d2.cpu().numpy(), "fwd_grad_d3.npz", "dtau_backgrad")
+    check(d2.detach().cpu().numpy(), "fwd_grad_d3.npz", "dtau_backgrad")
     # weights edited in place -> repacked
     with torch.no_grad():
         m.network.generator[4].bias.add_(0.5)
@@ -284,9 +284,9 @@ def test_arm_models_api(W, dev):
     m.network.to(dev)
     xp = T(a["xp"], dev)
     tau, coords = m.network.out(xp)
-    check(m.gradient(tau, coords).cpu().numpy(), "fwd_grad_d6.npz", "dtau")
+    check(m.gradient(tau, coords).detach().cpu().numpy(), "fwd_grad_d6.npz", "dtau")
     g = torch.cat([m.Gradient(xp[i:i + 1].clone()) for i in range(16)])
-    check(g.cpu().numpy(), "fwd_grad_d6.npz", "gradient16")
+    check(g.detach().cpu().numpy(), "fwd_grad_d6.npz", "gradient16")
 
 
 def test_large_batch_properties(packed, dev):
@@ -296,12 +296,12 @@ def test_large_batch_properties(packed, dev):
     xp = synth.make_pairs(n, 3, seed=2)
     B = synth.make_B(3, seed=1)
     t, d = ops.tau_grad(packed, T(xp, dev), T(B, dev), dim=3)
-    t, d = t.cpu().numpy(), d.cpu().numpy()
+    t, d = t.detach().cpu().numpy(), d.detach().cpu().numpy()
     assert np.isfinite(t).all() and np.isfinite(d).all() and (t > 0).all() and (t < 1).all()
     perm = np.random.default_rng(0).permutation(n)
     tp, dp = ops.tau_grad(packed, T(xp[perm], dev), T(B, dev), dim=3)
-    np.testing.assert_array_equal(tp.cpu().numpy(), t[perm])
-    np.testing.assert_array_equal(dp.cpu().numpy(), d[perm])
+    np.testing.assert_array_equal(tp.detach().cpu().numpy(), t[perm])
+    np.testing.assert_array_equal(dp.detach().cpu().numpy(), d[perm])
     idx = np.random.default_rng(1).choice(n, 512, replace=False)
     to, do = O.tau_grad(weights(), xp[idx], B)
     close(t[idx], to[:, 0], pairs=True)
@@ -320,11 +320,11 @@ def test_out_laplace_and_loss_vs_reference(W, dev):
     m.network.to(dev)
     pts, yobs, Bt = T(f["pts"], dev), T(f["yobs"], dev), T(f["B_table"], dev)
     tau, dtau, ltau, _ = m.network.out_laplace(pts, Bt)
-    check(tau.cpu().numpy(), "loss_d3.npz", "tau")
-    check(dtau.cpu().numpy(), "loss_d3.npz", "dtau")
-    check(ltau.cpu().numpy(), "loss_d3.npz", "ltau")
+    check(tau.detach().cpu().numpy(), "loss_d3.npz", "tau")
+    check(dtau.detach().cpu().numpy(), "loss_d3.npz", "dtau")
+    check(ltau.detach().cpu().numpy(), "loss_d3.npz", "ltau")
     loss, loss_n, diff = m.Loss(pts, yobs, Bt, 1.0, float(f["gamma"]))
-    check(diff.cpu().numpy(), "loss_d3.npz", "diff")
+    check(diff.detach().cpu().numpy(), "loss_d3.npz", "diff")
     assert abs(float(loss_n) - float(f["loss_n"])) < 1e-4 * abs(float(f["loss_n"]))
 
 
@@ -338,11 +338,11 @@ def test_arm_out_laplace_and_loss_vs_reference(W, dev):
     m.network.to(dev)
     pts = T(f["pts"], dev)
     tau, dtau, ltau, _ = m.network.out_laplace(pts)
-    check(tau.cpu().numpy(), "loss_d6.npz", "tau")
-    check(dtau.cpu().numpy(), "loss_d6.npz", "dtau")
-    check(ltau.cpu().numpy(), "loss_d6.npz", "ltau")
+    check(tau.detach().cpu().numpy(), "loss_d6.npz", "tau")
+    check(dtau.detach().cpu().numpy(), "loss_d6.npz", "dtau")
+    check(ltau.detach().cpu().numpy(), "loss_d6.npz", "ltau")
     _, loss_n, diff = m.Loss(pts, T(f["yobs"], dev), 1.0, float(f["gamma"]))
-    check(diff.cpu().numpy(), "loss_d6.npz", "diff")
+    check(diff.detach().cpu().numpy(), "loss_d6.npz", "diff")
 
 
 @pytest.mark.parametrize("n", [1, 17, 300])
@@ -354,10 +354,10 @@ def test_residual_ragged_vs_oracle(packed, dev, W, n):
     out = ops.eikonal_residual(packed, T(xp, dev), T(Bt, dev), T(env, dev, torch.int32), 3,
                                yobs=T(yobs, dev), gamma=1e-3)
     to, do, lo, dfo = O.eikonal_residual(W, xp, yobs, Bt, env, gamma=1e-3)
-    close(out["tau"].cpu().numpy(), to[:, 0], pairs=True)
-    close(out["dtau"].cpu().numpy(), do, pairs=True)
-    close(out["ltau"].cpu().numpy(), lo, pairs=True)
-    close(out["diff"].cpu().numpy(), dfo, pairs=True, diff=True)
+    close(out["tau"].detach().cpu().numpy(), to[:, 0], pairs=True)
+    close(out["dtau"].detach().cpu().numpy(), do, pairs=True)
+    close(out["ltau"].detach().cpu().numpy(), lo, pairs=True)
+    close(out["diff"].detach().cpu().numpy(), dfo, pairs=True, diff=True)
 
 
 def _elem_report(name, a, b):
@@ -403,7 +403,7 @@ def test_residual_grad_agrees_with_reverse_sweep(packed, dev, W):
     idx = np.random.default_rng(3).choice(n, 512, replace=False)
     to, do, lo, dfo = O.eikonal_residual(W, xp_np[idx], y_np[idx], Bt_np, env_np[idx],
                                          gamma=1e-3)
-    got = {k: v.cpu().numpy()[idx] for k, v in out.items()}
+    got = {k: v.detach().cpu().numpy()[idx] for k, v in out.items()}
     print("C3 1M sample vs fp64: " + "; ".join(
         _elem_report(k, got[k], r) for k, r in (("tau", to[:, 0]), ("dtau", do), ("ltau", lo),
                                                 ("diff", dfo))))
@@ -424,11 +424,11 @@ def test_residual_grad_agrees_with_reverse_sweep(packed, dev, W):
     # the 16-pair τ+∇τ kernel runs the same forward MFMA sequence: τ bit-identical
     t, d = ops.tau_grad(packed, xp, Bt, env, dim=3, schedule="wave_tile")
     assert torch.equal(out["tau"], t)
-    close(out["dtau"].cpu().numpy(), d.cpu().numpy(), tol=1e-5)
+    close(out["dtau"].detach().cpu().numpy(), d.detach().cpu().numpy(), tol=1e-5)
     # the 32-pair (wide) kernel sums in another order: fp32-rounding agreement
     tw, dw = ops.tau_grad(packed, xp, Bt, env, dim=3, schedule="wide_tile")
-    close(tw.cpu().numpy(), t.cpu().numpy(), tol=1e-6)
-    close(out["dtau"].cpu().numpy(), dw.cpu().numpy(), tol=1e-5)
+    close(tw.detach().cpu().numpy(), t.detach().cpu().numpy(), tol=1e-6)
+    close(out["dtau"].detach().cpu().numpy(), dw.detach().cpu().numpy(), tol=1e-5)
 
 
 def test_headline_1m_sample_vs_fp64_oracle(packed, dev, W):
@@ -444,7 +444,7 @@ def test_headline_1m_sample_vs_fp64_oracle(packed, dev, W):
     env_np = synth.make_env_ids(n, 10)
     assert ops.resolved_schedule(n) == "wide_tile"
     t, d = ops.tau_grad(packed, T(xp_np, dev), T(Bt_np, dev), T(env_np, dev, torch.int32), dim=3)
-    t, d = t.cpu().numpy(), d.cpu().numpy()
+    t, d = t.detach().cpu().numpy(), d.detach().cpu().numpy()
     assert np.isfinite(t).all() and np.isfinite(d).all() and (t > 0).all() and (t < 1).all()
     idx = np.random.default_rng(4).choice(n, 512, replace=False)
     to, do = O.tau_grad(W, xp_np[idx], Bt_np, env_np[idx])
@@ -486,8 +486,8 @@ def test_c4_shape_sharded_on_one_gpu(packed, dev, W):
         assert torch.equal(ts, t[lo:hi]) and torch.equal(dsh, d[lo:hi]), r
     idx = np.random.default_rng(8).choice(n, 256, replace=False)
     to, do = O.tau_grad(W, xp_np[idx], Bt_np, env_np[idx])
-    close(t.cpu().numpy()[idx], to[:, 0], pairs=True)
-    close(d.cpu().numpy()[idx], do, pairs=True)
+    close(t.detach().cpu().numpy()[idx], to[:, 0], pairs=True)
+    close(d.detach().cpu().numpy()[idx], do, pairs=True)
 
 
 def test_device_sum_deterministic(dev):
@@ -512,7 +512,7 @@ def test_planner_edge_cases(packed, dev, schedule, W):
         path, steps = ops.plan(packed, T(xp0, dev), T(Bt, dev), T(env, dev, torch.int32), dim=3,
                                step=1e-4, tol=0.06, max_iter=max_iter,
                                mode=ops.GRAD_BACKGRAD_COMPAT, schedule=schedule)
-        path, steps = path.cpu().numpy(), steps.cpu().numpy()
+        path, steps = path.detach().cpu().numpy(), steps.detach().cpu().numpy()
         assert path.shape == (q, max_iter + 2, 6)
         assert steps[3] == -1
         assert steps[1] == 0 and np.all(path[1] == xp0[1])
@@ -536,7 +536,7 @@ def test_single_query_planner_vs_reference(packed, dev, golden):
     for i in range(len(p["iters"])):
         path, steps = ops.plan(packed, T(p["starts"][i:i + 1], dev), B, **kw)
         assert int(steps.cpu()[0]) == int(p["iters"][i]), i
-        assert np.abs(path.cpu().numpy()[0] - p["paths"][i]).max() < 1e-3, i
+        assert np.abs(path.detach().cpu().numpy()[0] - p["paths"][i]).max() < 1e-3, i
 
 
 @pytest.mark.parametrize("dim,q", [(3, 37), (6, 200)])
@@ -566,10 +566,52 @@ def test_c5_tail_handoff_bitwise_and_taken(packed, dev):
     xq = T(synth.make_box_pairs(q, 6, seed=3), dev)
     kw = dict(dim=6, step=0.015, tol=0.03, max_iter=199, mode=ops.GRAD_EXACT)
     pa, sa = ops.plan(packed, xq, Ba, schedule="auto", **kw)
-    tail = ops._workspace(dev, q)[:8].view(torch.int32).cpu().numpy()
+    tail = ops._workspace(dev, q)[:8].view(torch.int32).detach().cpu().numpy()
     pq, sq = ops.plan(packed, xq, Ba, schedule="quad_tile", **kw)
     assert torch.equal(sa, sq)
     assert torch.equal(pa, pq), float((pa - pq).abs().max())
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     assert 0 < tail[1] <= cus, tail.tolist()          # handed-off queries
     assert tail[0] >= q - cus, tail.tolist()          # the done count that triggered it
+
+
+def test_net_handle_matches_packed_blob(packed, dev, W):
+    """The handle form of the C ABI (pntf_net_create / _update / _packed / _destroy) packs the
+    same weights as pntf_pack_weights: pntf_tau_grad on the handle's buffer is bitwise the
+    caller-owned blob's, and _update repacks after a weight change."""
+    import ctypes
+    from pntf import _lib
+    lib = _lib.load()
+    V = ctypes.c_void_p
+    params = [torch.from_numpy(v).to(dev) for v in W.values()]
+    arr = (V * 30)(*[p.data_ptr() for p in params])
+    s = V(torch.cuda.current_stream(dev).cuda_stream)
+    n = 333
+    xp = T(synth.make_pairs(n, 3, seed=7), dev)
+    B = T(synth.make_B(3), dev)
+    ws = torch.empty(int(lib.pntf_workspace_bytes(n)), dtype=torch.uint8, device=dev)
+
+    def run(packed_ptr):
+        t = torch.empty(n, device=dev)
+        d = torch.empty((n, 6), device=dev)
+        st = lib.pntf_tau_grad(V(packed_ptr), 3, V(xp.data_ptr()), n, V(B.data_ptr()), None, 1,
+                               0, V(t.data_ptr()), V(d.data_ptr()), V(ws.data_ptr()),
+                               ws.numel(), s)
+        assert st == 0, lib.pntf_last_error()
+        return t, d
+    h = lib.pntf_net_create(arr, 30, s)
+    assert h, lib.pntf_last_error()
+    try:
+        t0, d0 = run(packed.data_ptr())
+        t1, d1 = run(lib.pntf_net_packed(h))
+        assert torch.equal(t0, t1) and torch.equal(d0, d1)
+        params[5].mul_(1.5)                      # encoder.2.bias changes: repack both ways
+        assert lib.pntf_net_update(h, arr, 30, s) == 0
+        t2, d2 = run(lib.pntf_net_packed(h))
+        blob = ops.pack_weights(params)
+        t3, d3 = run(blob.data_ptr())
+        assert torch.equal(t2, t3) and torch.equal(d2, d3) and not torch.equal(t2, t0)
+    finally:
+        torch.cuda.synchronize()
+        lib.pntf_net_destroy(h)
+    assert not lib.pntf_net_create(None, 30, s) and b"null" in lib.pntf_last_error()

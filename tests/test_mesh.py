@@ -85,7 +85,7 @@ def test_hip_distance_matches_oracle(n, t):
     tris = random_mesh(rng, t).astype(np.float32)
     pts = rng.uniform(-0.5, 0.5, (n, 3)).astype(np.float32)
     d = ops.point_mesh_distance(torch.from_numpy(pts).cuda(),
-                                torch.from_numpy(tris).cuda()[None]).cpu().numpy()
+                                torch.from_numpy(tris).cuda()[None]).detach().cpu().numpy()
     ref = M.point_mesh_distance(pts, tris)
     assert d.shape == (n,)
     assert np.abs(d - ref).max() < TOL
@@ -104,7 +104,7 @@ def test_hip_distance_culling_on_large_sorted_query():
     b = ops.point_mesh_distance(P, T, order=False)
     assert torch.equal(a, b)
     sub = rng.choice(20000, 1500, replace=False)
-    assert np.abs(a.cpu().numpy()[sub] - M.point_mesh_distance(pts[sub], tris)).max() < TOL
+    assert np.abs(a.detach().cpu().numpy()[sub] - M.point_mesh_distance(pts[sub], tris)).max() < TOL
 
 
 @pytest.mark.gpu
@@ -129,7 +129,7 @@ def test_hip_distance_bits_independent_of_triangle_split():
     for c in (1, 3, 0):
         assert torch.equal(ops.point_mesh_distance(P, W, chunks=c, order=True), ref)
     sub = rng.choice(lat.shape[0], 1500, replace=False)
-    assert np.abs(ref.cpu().numpy()[sub] - M.point_mesh_distance(lat[sub], walls)).max() < TOL
+    assert np.abs(ref.detach().cpu().numpy()[sub] - M.point_mesh_distance(lat[sub], walls)).max() < TOL
 
 
 @pytest.mark.gpu
@@ -141,7 +141,7 @@ def test_hip_box_analytic_and_degenerate():
                            [[[0.0, 0, 0], [0.2, 0, 0], [0.1, 0, 0]]]]).astype(np.float32)
     pts = rng.uniform(-0.5, 0.5, (5000, 3)).astype(np.float32)
     d = ops.point_mesh_distance(torch.from_numpy(pts).cuda(),
-                                torch.from_numpy(tris).cuda()).cpu().numpy()
+                                torch.from_numpy(tris).cuda()).detach().cpu().numpy()
     assert np.all(np.isfinite(d))
     assert np.abs(d - M.point_mesh_distance(pts, tris)).max() < TOL
     assert ops.point_mesh_distance(torch.zeros(0, 3, device="cuda"),
@@ -171,4 +171,4 @@ def test_point_sampler_properties():
                                atol=TOL / margin)
     d = S.point_obstacle_distance(torch.from_numpy(X[:5, :3]).cuda(),
                                   torch.from_numpy(tris.astype(np.float32)).cuda()[None])
-    np.testing.assert_allclose(d.cpu().numpy(), d0[:5], atol=TOL)
+    np.testing.assert_allclose(d.detach().cpu().numpy(), d0[:5], atol=TOL)

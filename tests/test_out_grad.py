@@ -81,13 +81,13 @@ def test_out_weight_grads_vs_reference(tag, dim):
     B = f["B"] if dim == 3 else f["B"].T
     north_star_pairs("out_grad_%s_d%d tau" % (tag, dim), tau.detach().cpu().numpy()[:, 0],
                      f["tau"], O.forward(_weights(tag, dim), f["xp"], B, dim=dim)[:, 0])
-    assert _rel(coords.grad.cpu().numpy(), f["dcoords"]) < GRAD_TOL
+    assert _rel(coords.grad.detach().cpu().numpy(), f["dcoords"]) < GRAD_TOL
     for k, p in net.named_parameters():
         if k.startswith("encoder1.0."):
             assert p.grad is None, k            # never used (:160, :227): no gradient
         else:
             assert p.grad is not None, k
-            assert _rel(p.grad.cpu().numpy(), f["grad/" + k]) < GRAD_TOL, k
+            assert _rel(p.grad.detach().cpu().numpy(), f["grad/" + k]) < GRAD_TOL, k
 
 
 @pytest.mark.gpu
@@ -113,7 +113,7 @@ def test_out_weight_grads_accumulate_and_ragged():
             (tau[:, 0] * torch.from_numpy(wt).to(dev)).sum().backward()
         for k, p in net.named_parameters():
             if k in g:
-                assert _rel(p.grad.cpu().numpy(), 2.0 * g[k]) < GRAD_TOL, (n, k)
+                assert _rel(p.grad.detach().cpu().numpy(), 2.0 * g[k]) < GRAD_TOL, (n, k)
 
 
 @pytest.mark.gpu
@@ -137,7 +137,7 @@ def test_model_gradient_does_not_run_the_tape(monkeypatch):
     tau, coords = net.out(xp, B)
     d = model.gradient(tau, coords)
     assert calls == [] and all(p.grad is None for p in net.parameters())
-    _, d_ref = O.tau_grad(W, xp.cpu().numpy(), B.cpu().numpy())
+    _, d_ref = O.tau_grad(W, xp.detach().cpu().numpy(), B.detach().cpu().numpy())
     assert rel_l2(d.detach().cpu().numpy(), d_ref) < 1e-4
     with torch.no_grad():                      # no graph: no weight term at all
         t2, _ = net.out(xp, B)

@@ -135,7 +135,7 @@ def test_loss_backward_vs_reference(name, dim):
     for k, p in net.named_parameters():
         if "grad:" + k in f.files:
             assert p.grad is not None, k
-            assert _rel(p.grad.cpu().numpy(), f["grad:" + k]) < GRAD_TOL, k
+            assert _rel(p.grad.detach().cpu().numpy(), f["grad:" + k]) < GRAD_TOL, k
         else:
             assert p.grad is None, k            # encoder1.0: never used, no gradient
 
@@ -173,7 +173,7 @@ def test_two_adamw_steps_vs_reference(name, dim):
     for k in f.files:
         if k.startswith("after2:"):
             name = k[7:]
-            got = sd[name].cpu().numpy()
+            got = sd[name].detach().cpu().numpy()
             if name not in grads[0]:                 # encoder1.0: no gradient, unchanged
                 assert np.array_equal(got, f[k]), name
                 continue
@@ -183,7 +183,7 @@ def test_two_adamw_steps_vs_reference(name, dim):
             bound = 2e-6 + 8 * lr * delta / np.maximum(g, delta)
             worst = np.argmax(err - bound)
             assert (err <= bound).all(), (name, float(err.flat[worst]), float(bound.flat[worst]))
-    assert np.array_equal(sd["encoder1.0.weight"].cpu().numpy(), W["encoder1.0.weight"])
+    assert np.array_equal(sd["encoder1.0.weight"].detach().cpu().numpy(), W["encoder1.0.weight"])
 
 
 @pytest.mark.gpu
@@ -259,9 +259,9 @@ def test_weight_grads_ragged_multi_env_vs_oracle(n):
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
     diff = train.loss_grad(params, T(xp), T(yobs), T(Bt), T(env), 3, 1e-3, 1.0 / n, False,
                            grads)
-    assert _rel(diff.cpu().numpy(), diff_o) < 1e-4
+    assert _rel(diff.detach().cpu().numpy(), diff_o) < 1e-4
     for k in params:
-        assert _rel(grads[k].cpu().numpy(), g_o[k]) < GRAD_TOL, k
+        assert _rel(grads[k].detach().cpu().numpy(), g_o[k]) < GRAD_TOL, k
 
 
 @pytest.mark.gpu
@@ -278,7 +278,7 @@ def test_training_loss_matches_inference_loss():
     _, ln1, d1 = model.Loss(T(f["pts"]), T(f["yobs"]), T(f["B_table"]), 1.0, 1e-3)
     assert ln1.requires_grad and not ln0.requires_grad
     assert abs(ln0.item() - ln1.item()) < 1e-5 * max(1.0, abs(ln0.item()))
-    assert _rel(d1.detach().cpu().numpy(), d0.cpu().numpy()) < 1e-4
+    assert _rel(d1.detach().cpu().numpy(), d0.detach().cpu().numpy()) < 1e-4
     assert md is not None
 
 
@@ -485,8 +485,8 @@ def test_fused_linear_act_ragged_vs_two_kernel(fused, dim, n, monkeypatch):
     assert torch.allclose(d1, d2, rtol=1e-5, atol=1e-5)
     assert torch.allclose(t1, t2, rtol=1e-6, atol=1e-7)
     for k in params:
-        assert _rel(g1[k].cpu().numpy(), g2[k].cpu().numpy()) < 1e-5, k
-        assert _rel(v1[k].cpu().numpy(), v2[k].cpu().numpy()) < 1e-5, k
+        assert _rel(g1[k].detach().cpu().numpy(), g2[k].detach().cpu().numpy()) < 1e-5, k
+        assert _rel(v1[k].detach().cpu().numpy(), v2[k].detach().cpu().numpy()) < 1e-5, k
 
 
 @pytest.mark.gpu

@@ -177,7 +177,7 @@ def run_method(net, model, calls, f, meth, dim, dev):
         loss = (wt * tau).sum() + (wd * dtau).sum()
         leaf = x
     loss.backward()
-    dc = leaf.grad.cpu().numpy() if leaf.grad is not None else None
+    dc = leaf.grad.detach().cpu().numpy() if leaf.grad is not None else None
     return tau.detach().cpu().numpy(), dtau.detach().cpu().numpy(), lt, dc
 
 
@@ -202,7 +202,7 @@ def test_drop_in_vjp_vs_reference(tag, dim, meth):
     assert dc is not None, "coords received no gradient"
     e_dc = float(np.abs(dc - f[meth + "/dcoords"]).max() / np.abs(f[meth + "/dcoords"]).max())
     assert e_dc < GRAD_TOL, (meth, e_dc)
-    grads = {k: (p.grad.cpu().numpy() if p.grad is not None else None)
+    grads = {k: (p.grad.detach().cpu().numpy() if p.grad is not None else None)
              for k, p in net.named_parameters()}
     worst = check_grads(f, meth, grads, GRAD_TOL)
     print("%s %s d%d: coords %.2e, worst param %.2e" % (meth, tag, dim, e_dc, worst))
@@ -234,13 +234,13 @@ def test_field_vjp_ragged_env_table_vs_oracle(n, nle):
     k = {"none": 0, "sum": 1, "dir": 3}[nle]
     gx = train.field_vjp(p, cuda(xp), cuda(Bt), torch.from_numpy(env).to(dev), 3, k, False,
                          cuda(gt), cuda(gd), glap, grads, True)
-    assert float(np.abs(gx.cpu().numpy() - dxo).max() / np.abs(dxo).max()) < GRAD_TOL
+    assert float(np.abs(gx.detach().cpu().numpy() - dxo).max() / np.abs(dxo).max()) < GRAD_TOL
     for key, g in grads.items():
         r = go[key]
         # the head bias gradient is one sum over the pairs of ±-weighted terms and can cancel
         # to far below its terms: it is held relative to the head weight gradient's scale
         scale = np.abs(go["generator.4.weight"]).max() if r.size == 1 else np.abs(r).max()
-        assert float(np.abs(g.cpu().numpy() - r).max() / scale) < GRAD_TOL, key
+        assert float(np.abs(g.detach().cpu().numpy() - r).max() / scale) < GRAD_TOL, key
 
 
 @pytest.mark.gpu

@@ -149,16 +149,16 @@ def test_w2_drop_in_load_and_fields(multi):
     xp, B = _T(f["xp"], dev), _T(f["B"], dev)
     tau, coords = multi.network.out(xp, B)
     check(tau.detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "tau")
-    check(multi.gradient(tau, coords).cpu().numpy(), "fwd_grad_w2_d3.npz", "dtau")
+    check(multi.gradient(tau, coords).detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "dtau")
     _, d1, _ = multi.network.out_grad(xp, B)
-    check(d1.cpu().numpy(), "fwd_grad_w2_d3.npz", "dtau_fwdmode")
+    check(d1.detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "dtau_fwdmode")
     t2, d2, _ = multi.network.out_backgrad(xp, B)
-    check(t2.cpu().numpy(), "fwd_grad_w2_d3.npz", "tau_backgrad")
-    check(d2.cpu().numpy(), "fwd_grad_w2_d3.npz", "dtau_backgrad")
-    check(multi.Gradient(xp.clone(), B).cpu().numpy(), "fwd_grad_w2_d3.npz", "gradient")
+    check(t2.detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "tau_backgrad")
+    check(d2.detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "dtau_backgrad")
+    check(multi.Gradient(xp.clone(), B).detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "gradient")
     multi.B = B
-    check(multi.Speed(xp).cpu().numpy(), "fwd_grad_w2_d3.npz", "speed")
-    check(multi.TravelTimes(xp).cpu().numpy(), "fwd_grad_w2_d3.npz", "travel_time")
+    check(multi.Speed(xp).detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "speed")
+    check(multi.TravelTimes(xp).detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "travel_time")
 
 
 @pytest.mark.gpu
@@ -170,8 +170,8 @@ def test_w2_field_schedules(multi, schedule):
     f = load("fwd_grad_w2_d3.npz")
     t, d = ops.tau_grad(multi.network.packed(), _T(f["xp"], dev), _T(f["B"], dev), dim=3,
                         schedule=schedule)
-    check(t.cpu().numpy(), "fwd_grad_w2_d3.npz", "tau")
-    check(d.cpu().numpy(), "fwd_grad_w2_d3.npz", "dtau")
+    check(t.detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "tau")
+    check(d.detach().cpu().numpy(), "fwd_grad_w2_d3.npz", "dtau")
 
 
 @pytest.mark.gpu
@@ -181,21 +181,21 @@ def test_w2_laplace_and_loss(multi, arm):
     f = load("loss_w2_d3.npz")
     pts, Bt = _T(f["pts"], dev), _T(f["B_table"], dev)
     tau, dtau, ltau, _ = multi.network.out_laplace(pts, Bt)
-    check(tau.cpu().numpy(), "loss_w2_d3.npz", "tau")
-    check(dtau.cpu().numpy(), "loss_w2_d3.npz", "dtau")
-    check(ltau.cpu().numpy(), "loss_w2_d3.npz", "ltau")
+    check(tau.detach().cpu().numpy(), "loss_w2_d3.npz", "tau")
+    check(dtau.detach().cpu().numpy(), "loss_w2_d3.npz", "dtau")
+    check(ltau.detach().cpu().numpy(), "loss_w2_d3.npz", "ltau")
     with torch.no_grad():
         _, loss_n, diff = multi.Loss(pts, _T(f["yobs"], dev), Bt, 1.0, float(f["gamma"]))
-    check(diff.cpu().numpy(), "loss_w2_d3.npz", "diff")
+    check(diff.detach().cpu().numpy(), "loss_w2_d3.npz", "diff")
     assert abs(float(loss_n) - float(f["loss_n"])) < 1e-4 * abs(float(f["loss_n"]))
     g = load("loss_w2_d6.npz")
     pts = _T(g["pts"], dev)
     tau, dtau, ltau, _ = arm.network.out_laplace(pts)
-    check(dtau.cpu().numpy(), "loss_w2_d6.npz", "dtau")
-    check(ltau.cpu().numpy(), "loss_w2_d6.npz", "ltau")
+    check(dtau.detach().cpu().numpy(), "loss_w2_d6.npz", "dtau")
+    check(ltau.detach().cpu().numpy(), "loss_w2_d6.npz", "ltau")
     with torch.no_grad():
         _, _, diff = arm.Loss(pts, _T(g["yobs"], dev), 1.0, float(g["gamma"]))
-    check(diff.cpu().numpy(), "loss_w2_d6.npz", "diff")
+    check(diff.detach().cpu().numpy(), "loss_w2_d6.npz", "diff")
 
 
 @pytest.mark.gpu
@@ -203,13 +203,13 @@ def test_w2_arm_fields(arm):
     from test_gpu_parity import check, close
     dev = torch.device("cuda:0")
     a = load("fwd_grad_w2_d6.npz")
-    np.testing.assert_array_equal(arm.B.cpu().numpy(), a["B"])      # B_state_dict restored
+    np.testing.assert_array_equal(arm.B.detach().cpu().numpy(), a["B"])      # B_state_dict restored
     xp = _T(a["xp"], dev)
     tau, coords = arm.network.out(xp)
     check(tau.detach().cpu().numpy(), "fwd_grad_w2_d6.npz", "tau")
-    check(arm.gradient(tau, coords).cpu().numpy(), "fwd_grad_w2_d6.npz", "dtau")
+    check(arm.gradient(tau, coords).detach().cpu().numpy(), "fwd_grad_w2_d6.npz", "dtau")
     g = torch.cat([arm.Gradient(xp[i:i + 1].clone()) for i in range(16)])
-    check(g.cpu().numpy(), "fwd_grad_w2_d6.npz", "gradient16")
+    check(g.detach().cpu().numpy(), "fwd_grad_w2_d6.npz", "gradient16")
 
 
 @pytest.mark.gpu
@@ -221,14 +221,14 @@ def test_w2_planners_vs_reference(multi, arm, schedule):
     path, steps = ops.plan(multi.network.packed(), _T(p["starts"], dev), _T(p["B"], dev),
                            dim=3, step=0.03, tol=0.06, max_iter=500,
                            mode=ops.GRAD_BACKGRAD_COMPAT, schedule=schedule)
-    np.testing.assert_array_equal(steps.cpu().numpy(), p["iters"])
-    assert np.abs(path.cpu().numpy() - p["paths"]).max() < 1e-3
+    np.testing.assert_array_equal(steps.detach().cpu().numpy(), p["iters"])
+    assert np.abs(path.detach().cpu().numpy() - p["paths"]).max() < 1e-3
     a = load("plan_arm_w2.npz")
     path, steps = ops.plan(arm.network.packed(), _T(a["starts"], dev), _T(a["B"].T, dev),
                            dim=6, step=0.015, tol=0.03, max_iter=300, mode=ops.GRAD_EXACT,
                            schedule=schedule)
-    np.testing.assert_array_equal(steps.cpu().numpy(), a["iters"])
-    assert np.abs(path.cpu().numpy() - a["paths"]).max() < 1e-3
+    np.testing.assert_array_equal(steps.detach().cpu().numpy(), a["iters"])
+    assert np.abs(path.detach().cpu().numpy() - a["paths"]).max() < 1e-3
 
 
 def c5_envelope_check(steps, fin, ref_iters, ref_final, f64_iters, f64_final, drift=None,
@@ -305,7 +305,7 @@ def test_w2_c5_1024_queries_vs_reference(arm):
     c, f64 = load("plan_c5_w2.npz"), load("plan_c5_w2_fp64.npz")
     tol = float(c["tol"])
     path, steps = arm.Plan(_T(c["xq"], dev), step=0.015, tol=tol, max_iter=int(c["max_iter"]))
-    path, steps = path.cpu().numpy(), steps.cpu().numpy()
+    path, steps = path.detach().cpu().numpy(), steps.detach().cpu().numpy()
     q = np.arange(len(steps))
     fin = path[q, steps]
     dist = np.linalg.norm(fin[:, 6:] - fin[:, :6], axis=1)
@@ -342,4 +342,4 @@ def test_w2_single_query_planners_vs_reference(multi, arm):
             path, steps = ops.plan(net.network.packed(), _T(f["starts"][i:i + 1], dev),
                                    _T(B(f), dev), **kw)
             assert int(steps.cpu()[0]) == int(f["iters"][i]), (name, i)
-            assert np.abs(path.cpu().numpy()[0] - f["paths"][i]).max() < 1e-3, (name, i)
+            assert np.abs(path.detach().cpu().numpy()[0] - f["paths"][i]).max() < 1e-3, (name, i)

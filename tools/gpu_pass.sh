@@ -5,7 +5,8 @@
 #   tools/gpu_pass.sh <tag> <step>...
 #
 # steps (each under its own time limit, chained: the first failure ends the pass):
-#   tests[=<pytest args>]  the -m gpu suite (default: all of tests/), log <tag>_gpu_tests.log
+#   tests[=<pytest args>]  the -m gpu suite (default: all of tests/), log <tag>_gpu_tests.log;
+#                          alltests[=...] runs past failures (reports them, goes on)
 #   bench                  the default bench.py line -> <tag>_bench.json
 #   head                   headline kernel: rocprofv3 stats over 20 steps + FETCH/WRITE/MFMA/
 #                          stall PMC passes (tools/profile_round.sh) -> <tag>_prof/
@@ -28,11 +29,19 @@ cd "$R"
 for step in "$@"; do
   echo "== $step $(date +%T)"
   case "$step" in
-    tests*)
-      args=${step#tests}; args=${args#=}; [ -z "$args" ] && args=tests
-      timeout -k 10 900 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread \
-        -m gpu $args > "$OUT/${TAG}_gpu_tests.log" 2>&1 || { tail -60 "$OUT/${TAG}_gpu_tests.log"; exit 1; }
-      tail -3 "$OUT/${TAG}_gpu_tests.log" ;;
+    tests*|alltests*)
+      # tests: stop at the first failure and end the pass; alltests: run every test, report
+      # the failures and go on (kernel faults still end the pass: their exit status is not 1)
+      x=-x; [ "${step#all}" != "$step" ] && x=; s0=${step#all}
+      args=${s0#tests}; args=${args#=}; [ -z "$args" ] && args=tests
+      rc=0
+      timeout -k 10 1200 python -u -m pytest $x -v -s --timeout 300 --timeout-method thread \
+        -m gpu $args > "$OUT/${TAG}_gpu_tests.log" 2>&1 || rc=$?
+      tail -3 "$OUT/${TAG}_gpu_tests.log"
+      if [ $rc -ne 0 ]; then
+        grep -E "^FAILED|^ERROR" "$OUT/${TAG}_gpu_tests.log" | head -40
+        [ -n "$x" ] || [ $rc -ne 1 ] && exit 1
+      fi ;;
     bench)
       timeout -k 10 900 python3 bench.py > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err" \
         || { tail -30 "$OUT/${TAG}_bench.err"; exit 1; }

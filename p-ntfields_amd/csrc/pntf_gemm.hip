@@ -25,6 +25,7 @@
 #include <stdlib.h>
 
 #include "pntf.h"
+#include "pntf_stamp.h"
 
 namespace pntf_gemm {
 
@@ -454,6 +455,7 @@ __global__ __launch_bounds__(256, PNTF_PANEL_WPS) void panel_gemm_kernel(PanelAr
 // panel read of a tile hits that XCD's L2.
 template <int KC, int NC, bool ACC>
 __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
+  PNTF_CLOCK_SCOPE;
   constexpr int QK = KC / 8, NG = NC / 128, FR = 4 * QK;
   static_assert(QK >= 8, "C prefetch distance");
   __shared__ f32x4 lw[FR * 64];
@@ -1060,6 +1062,7 @@ __device__ __forceinline__ void wg_store(float* p, f32x4 v) {
 
 template <int T, int NB>
 __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs g) {
+  PNTF_CLOCK_SCOPE;
   __shared__ f32x4 red[2][64 * 64];   // two 128 x 128 tiles (128 KiB)
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

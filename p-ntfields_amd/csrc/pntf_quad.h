@@ -31,6 +31,7 @@
 // lane consumes (τ, ∇τ) use xor butterflies and a fixed wave order, so all lanes of a pair
 // hold bitwise identical values and the planner's freeze/exit decisions agree in all waves.
 #include "pntf_split.h"
+#include "pntf_stamp.h"
 
 namespace pntf {
 
@@ -667,6 +668,7 @@ static_assert(Q_YIELD_FLAG < Q_LDS_FLOATS, "quad LDS budget");
 
 template <int DIM, bool SOLO>
 __global__ __launch_bounds__(64 * Q_WAVES, 1) void plan_quad_kernel(PlanArgs a) {
+  PNTF_CLOCK_SCOPE;
   __shared__ float smem[Q_LDS_FLOATS];
   const QCx cx = quad_cx((lds_f*)smem);
   int32_t* const tail = a.tail;

@@ -23,6 +23,7 @@
 //   * activations live in two banks X[8], Y[8] (256 features, or 2 points x 128 features);
 //     saved σ10 tiles (4 KiB per 32-feature tile and point) go to a per-wave scratch slot.
 #include "pntf_field.h"
+#include "pntf_stamp.h"
 
 namespace pntf {
 
@@ -72,6 +73,10 @@ __device__ __forceinline__ WScratch make_wscratch(float* p) {
 #ifdef PNTF_ABL_HOTLOAD   // diagnostics only: σ reloads from a 16 KiB region no store touches
 __device__ float pntf_abl_hot[4 * 1024];
 #endif
+// cache policy of the saved-σ stores (nt: they stream past the L2 that holds the weights)
+#ifndef PNTF_WSTORE_AUX
+#define PNTF_WSTORE_AUX AUX_NT
+#endif
 // tile t = 4 KiB: part q (registers 4q..4q+3) of all lanes is 1 KiB contiguous
 __device__ __forceinline__ void wstore(WScratch sc, int t, int lane, const f32x16& v) {
 #ifdef PNTF_ABL_NOSTORE   // diagnostics only: the σ stores are dropped (wrong results)
@@ -81,7 +86,7 @@ __device__ __forceinline__ void wstore(WScratch sc, int t, int lane, const f32x1
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     f32x4 p{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
-    bstore<AUX_NT>(sc.r, p, lane * 16, t * 4096 + q * 1024);
+    bstore<PNTF_WSTORE_AUX>(sc.r, p, lane * 16, t * 4096 + q * 1024);
   }
 }
 __device__ __forceinline__ f32x16 wload(WScratch sc, int t, int lane) {
@@ -660,6 +665,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
 // ---------------------------------------------------------------- kernel
 template <int DIM, int KIND, bool BL>
 __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
+  PNTF_CLOCK_SCOPE;
   constexpr bool GRAD = KIND != K_TAU && KIND != K_TRAVEL;
   const int lane = threadIdx.x & 63;
   const int slot = blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -529,15 +529,13 @@ TRAIN_FLOP_EXECUTED_PER_PAIR = 3 * 2 * (2 * 5 * 114_688 + 9 * 425_984)
 
 def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=20, warm=5):
     """Model.train inner step (model_res_sigmoid_multi.py:1040-1052) on the HIP Taylor tape:
-    Loss forward + loss.backward() + AdamW step, as Model.train runs it: Loss + backward
-    replayed from a HIP graph (pntf/train.py GraphedLoss), then the one-launch AdamW
-    (`_eager_ms`: the same step launched kernel by kernel).  (2, 10000) is the reference's
-    batch (Batch Size 2 environments x inner_batch 10000 pairs, :1010-1036).  `warm` untimed
+    Loss forward + loss.backward() + AdamW step, as Model.train runs it.  (2, 10000) is the
+    reference's batch (Batch Size 2 environments x inner_batch 10000 pairs, :1010-1036).  `warm` untimed
     steps first: after the host syncs of the legs before it the GPU clock ramps back over the
     first few launches, which one warm-up step does not cover."""
     from models import model_res_sigmoid_multi as md
     from pntf import synth
-    from pntf.train import AdamW, GraphedLoss
+    from pntf.train import AdamW
     out = {}
     W = synth.make_weights(0)
     net = md.NN(dev, 3)
@@ -556,13 +554,6 @@ def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=20, warm=5):
             loss.backward()
             opt.step()
             opt.zero_grad()
-        # what Model.train runs: Loss + backward replayed from a HIP graph, then AdamW
-        gl = GraphedLoss(lambda x, y, b, bt: model.Loss(x, y, b, bt, 1e-3), net.parameters())
-
-        def graphed():
-            gl(pts, yobs, Bt, beta=1.0, key=1e-3)
-            opt.step()
-            opt.zero_grad()
 
         def per_step(fn):
             for _ in range(warm):
@@ -574,8 +565,7 @@ def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=20, warm=5):
             torch.cuda.synchronize()
             return (time.perf_counter() - t0) / reps * 1e3
         tag = "train_step_%dx%d" % (E, n)
-        out[tag + "_eager_ms"] = per_step(eager)
-        ms = per_step(graphed)
+        ms = per_step(eager)
         out[tag + "_ms"] = ms
         out[tag + "_pairs_per_s"] = E * n / (ms * 1e-3)
         out[tag + "_TFLOPs_reference_equivalent"] = TRAIN_FLOP_PER_PAIR * E * n / (ms * 1e-3) / 1e12

@@ -1460,7 +1460,15 @@ static int tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float*
   return PNTF_OK;
 }
 
-extern "C" int pntf_tt_planes_ok(int ndir, int nl);
+// pntf_train.hip defines the plane check (its with_planes list); this weak copy of the list
+// only serves a standalone build of this file (tests/diag/build_gemm.sh)
+extern "C" __attribute__((weak, visibility("hidden"))) int pntf_tt_planes_ok(int ndir, int nl) {
+  const int ok[][2] = {{0, 0}, {3, 1}, {6, 1}, {6, 2}, {12, 2}, {3, 0},
+                       {6, 0}, {12, 0}, {3, 3}, {6, 6}, {12, 12}};
+  for (const auto& p : ok)
+    if (p[0] == ndir && p[1] == nl) return 1;
+  return 0;
+}
 
 int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const float* W,
                        int n, const float* bias, const float* res, float* y, float* h, int act,

@@ -194,11 +194,11 @@ class Model:
                                           shuffle=True)
         beta, prev_diff, current_diff = 1.0, 1.0, 1.0
         step = -2000.0 / 4000.0
-        # the inner step's Loss + backward as one HIP graph replay (pntf/train.py GraphedLoss);
-        # Params["Training"]["HIP Graph (bool)"] = False runs it eagerly
+        # Params["Training"]["HIP Graph (bool)"] = True replays the inner step's Loss + backward
+        # from one HIP graph (pntf/train.py GraphedLoss); off by default
         graphed = (_train.GraphedLoss(lambda x, y, bt: self.Loss(x, y, bt, gamma),
                                       self.network.parameters())
-                   if P["Training"].get("HIP Graph (bool)", True) else None)
+                   if P["Training"].get("HIP Graph (bool)", False) else None)
         current_state = copy.deepcopy(self.network.state_dict())
         current_optimizer = copy.deepcopy(self.optimizer.state_dict())
         prev_state_queue, prev_optimizer_queue = [], []

@@ -228,11 +228,11 @@ class Model:
         current_optimizer = copy.deepcopy(self.optimizer.state_dict())
         prev_state_queue, prev_optimizer_queue = [], []
         inner_batch = int(P["Training"].get("Inner Batch", 10000))
-        # the inner step's Loss + backward as one HIP graph replay (pntf/train.py GraphedLoss);
-        # Params["Training"]["HIP Graph (bool)"] = False runs it eagerly
+        # Params["Training"]["HIP Graph (bool)"] = True replays the inner step's Loss + backward
+        # from one HIP graph (pntf/train.py GraphedLoss); off by default
         graphed = (_train.GraphedLoss(lambda x, y, b, bt: self.Loss(x, y, b, bt, gamma),
                                       self.network.parameters())
-                   if P["Training"].get("HIP Graph (bool)", True) else None)
+                   if P["Training"].get("HIP Graph (bool)", False) else None)
         inner_rows = self.dataset[0][0].shape[0]
         inner_size = max(1, int(inner_rows / inner_batch))
         for epoch in range(1, P["Training"]["Number of Epochs"] + 1):

@@ -328,3 +328,27 @@ def test_fused_bwd_multi_round_matches_two_kernel():
     for k in p:
         a, b = out[0][1][k], out[1][1][k]
         assert float((a - b).abs().max() / b.abs().max()) < 1e-4, k
+
+
+@pytest.mark.gpu
+def test_arm_speed2_vs_oracle():
+    """Arm Model.Speed2 (models/model_res_sigmoid.py:1218-1245: the speed at the goal with the
+    viscosity term from out_laplace) against the fp64 oracle's Taylor mode, per pair 1e-4."""
+    from golden_util import north_star_pairs
+    from models import model_res_sigmoid as ma
+    dev = torch.device("cuda:0")
+    W = _weights("w2", 6)
+    sd = torch.load(os.path.join(GOLDEN, "ckpt_w2_d6.pt"), map_location="cpu",
+                    weights_only=True)
+    m = ma.Model(".", ".", 6, device=dev)
+    m.load(os.path.join(GOLDEN, "ckpt_w2_d6.pt"))
+    xp = synth.make_box_pairs(100, 6, seed=80)
+    gamma = 1e-3
+    v = m.Speed2(torch.from_numpy(xp).to(dev), gamma).detach().cpu().numpy()
+    t, d, lt = O.laplace(W, xp, sd["B_state_dict"].numpy().T, dim=6)
+    D = xp[:, 6:] - xp[:, :6]
+    T0 = (D * D).sum(1)
+    t = t[:, 0]
+    S = T0 * (d[:, 6:] ** 2).sum(1) - 2 * t * (d[:, 6:] * D).sum(1) + t * t
+    ref = 1.0 / (np.sqrt(S) / (t * t) + gamma * lt[:, 6:].sum(1))
+    north_star_pairs("arm Speed2", v, ref, ref)

@@ -61,6 +61,11 @@ constexpr int QRING_TAU = 64 / Q_WAVES;
 #ifndef PNTF_QPIN
 #define PNTF_QPIN 1
 #endif
+// cache policy of the weight-stream loads (every CU reads the same fragments from L2 once per
+// step; the CU's L1 never sees a fragment twice)
+#ifndef PNTF_QLOAD_AUX
+#define PNTF_QLOAD_AUX 0
+#endif
 // stream position (mod the ring) of a layer that follows a 128 x 128 one: the first ring slot
 // of every other encoder layer
 constexpr int QH = 64 / Q_WAVES;
@@ -210,7 +215,8 @@ __device__ __forceinline__ void qfetch(QRing<QR>& ring, Rsrc W, int lane, int sl
 #ifdef PNTF_QABL_NOLOAD   // diagnostics only (tests/diag timing ablations; wrong results)
   ring.r[slot] = ring.r[slot] * 1.0001f;
 #else
-  ring.r[slot] = bload(W, lane * 16, ring.off);
+  ring.r[slot] = __builtin_bit_cast(
+      f32x4, __builtin_amdgcn_raw_buffer_load_b128(W, lane * 16, ring.off, PNTF_QLOAD_AUX));
 #endif
   ring.off += 1024;
 #if PNTF_QPIN

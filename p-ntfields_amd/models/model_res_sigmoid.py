@@ -194,11 +194,6 @@ class Model:
                                           shuffle=True)
         beta, prev_diff, current_diff = 1.0, 1.0, 1.0
         step = -2000.0 / 4000.0
-        # Params["Training"]["HIP Graph (bool)"] = True replays the inner step's Loss + backward
-        # from one HIP graph (pntf/train.py GraphedLoss); off by default
-        graphed = (_train.GraphedLoss(lambda x, y, bt: self.Loss(x, y, bt, gamma),
-                                      self.network.parameters())
-                   if P["Training"].get("HIP Graph (bool)", False) else None)
         current_state = copy.deepcopy(self.network.state_dict())
         current_optimizer = copy.deepcopy(self.optimizer.state_dict())
         prev_state_queue, prev_optimizer_queue = [], []
@@ -226,11 +221,8 @@ class Model:
                     data = data[0]
                     points = data[:, :2 * self.dim].contiguous()
                     speed = (alpha * data[:, 2 * self.dim:] + 1 - alpha).contiguous()
-                    if graphed is not None:   # Loss + backward replayed from a HIP graph
-                        loss_value, loss_n, _ = graphed(points, speed, beta=beta, key=gamma)
-                    else:
-                        loss_value, loss_n, _ = self.Loss(points, speed, beta, gamma)
-                        loss_value.backward()
+                    loss_value, loss_n, _ = self.Loss(points, speed, beta, gamma)
+                    loss_value.backward()
                     self.optimizer.step()
                     self.optimizer.zero_grad()
                     total_train_loss += loss_value.detach()

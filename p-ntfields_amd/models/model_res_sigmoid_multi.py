@@ -228,11 +228,6 @@ class Model:
         current_optimizer = copy.deepcopy(self.optimizer.state_dict())
         prev_state_queue, prev_optimizer_queue = [], []
         inner_batch = int(P["Training"].get("Inner Batch", 10000))
-        # Params["Training"]["HIP Graph (bool)"] = True replays the inner step's Loss + backward
-        # from one HIP graph (pntf/train.py GraphedLoss); off by default
-        graphed = (_train.GraphedLoss(lambda x, y, b, bt: self.Loss(x, y, b, bt, gamma),
-                                      self.network.parameters())
-                   if P["Training"].get("HIP Graph (bool)", False) else None)
         inner_rows = self.dataset[0][0].shape[0]
         inner_size = max(1, int(inner_rows / inner_batch))
         for epoch in range(1, P["Training"]["Number of Epochs"] + 1):
@@ -271,11 +266,8 @@ class Model:
                         sl = slice(ii * inner_batch, (ii + 1) * inner_batch)
                         bp, bs = points_sh[:, sl].contiguous(), speed_sh[:, sl].contiguous()
                         self.B = B[0, :]
-                        if graphed is not None:   # Loss + backward replayed from a HIP graph
-                            loss_value, loss_n, _ = graphed(bp, bs, B, beta=beta, key=gamma)
-                        else:
-                            loss_value, loss_n, _ = self.Loss(bp, bs, B, beta, gamma)
-                            loss_value.backward()
+                        loss_value, loss_n, _ = self.Loss(bp, bs, B, beta, gamma)
+                        loss_value.backward()
                         self.optimizer.step()
                         self.optimizer.zero_grad()
                         total_train_loss += loss_value.detach()

@@ -501,59 +501,3 @@ class AdamW(torch.optim.Optimizer):
                 torch.autograd.graph.increment_version(t[0])
         return loss
 
-
-class GraphedLoss:
-    """One inner training step's `loss = Model.Loss(...)` + `loss.backward()`
-    (models/model_res_sigmoid_multi.py:1040-1048; arm models/model_res_sigmoid.py:1062-1071),
-    captured once into a HIP graph (torch.cuda.CUDAGraph) and replayed: the ~150 launches of
-    the Taylor tape become one graph launch.  The batch tensors and beta are copied into the
-    graph's static inputs before each replay (beta as a device scalar, so the epoch's 1/loss
-    rescaling reaches the gradients); the weights are read in place, so load_state_dict (the
-    reference's rollback) needs no re-capture.  After a replay every trained parameter's
-    `.grad` is the graph's gradient buffer (re-attached if optimizer.zero_grad() set it to
-    None).  A change of input shapes, device or `key` (gamma) re-captures.
-
-    loss_fn(*inputs, beta) -> (loss, loss_n, diff).  Returns the graph's static outputs
-    (valid until the next call)."""
-
-    def __init__(self, loss_fn, params):
-        self.loss_fn = loss_fn
-        self.params = [p for p in params if p.requires_grad]
-        self.graph = None
-        self.key = None
-
-    def _capture(self, inputs, beta):
-        dev = inputs[0].device
-        self.st = [x.clone() for x in inputs]
-        self.beta_t = torch.full((), float(beta), dtype=torch.float32, device=dev)
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):            # warm-up outside the capture (allocations)
-            for _ in range(2):
-                for p in self.params:
-                    p.grad = None
-                self.loss_fn(*self.st, self.beta_t)[0].backward()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        for p in self.params:
-            p.grad = None
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.out = self.loss_fn(*self.st, self.beta_t)
-            self.out[0].backward()
-        self.grads = [p.grad for p in self.params]
-        self.graph = g
-
-    def __call__(self, *inputs, beta=1.0, key=None):
-        k = (tuple(tuple(x.shape) for x in inputs), inputs[0].device, key)
-        if self.graph is None or k != self.key:
-            self.graph = None
-            self._capture(inputs, beta)
-            self.key = k
-        for dst, src in zip(self.st, inputs):
-            dst.copy_(src)
-        self.beta_t.fill_(float(beta))
-        self.graph.replay()
-        for p, gr in zip(self.params, self.grads):
-            if p.grad is None or p.grad.data_ptr() != gr.data_ptr():
-                p.grad = gr
-        return self.out

@@ -613,46 +613,3 @@ def test_panel_gemm_fallbacks_vs_fp64(case):
     err = (C.cpu().double() - ref).abs()
     assert torch.all(err <= 1e-5 * np.sqrt(K) * scale + 1e-6), float((err / scale).max())
 
-
-@pytest.mark.gpu
-@pytest.mark.skipif(os.environ.get("PNTF_TEST_GRAPHS") != "1",
-                    reason="HIP graph capture of the tape segfaulted in hipStreamEndCapture on "
-                           "the pool's ROCm build (profiles/r05_graph_capture.txt); opt-in")
-def test_graphed_loss_matches_eager():
-    """GraphedLoss (the HIP-graph replay Model.train uses for Loss + backward) gives bitwise
-    the eager step's loss, residuals and weight gradients, for a new batch and beta on every
-    replay, and re-attaches .grad after optimizer.zero_grad() sets it to None."""
-    from models import model_res_sigmoid_multi as md
-    from pntf.train import AdamW, GraphedLoss
-    dev = torch.device("cuda:0")
-    net = md.NN(dev, 3)
-    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.make_weights(0).items()})
-    net.to(dev)
-    model = md.Model(".", ".", 3, 2, device=dev)
-    model.network = net
-    opt = AdamW(net.parameters(), lr=1e-3, weight_decay=0.1)
-    E, n = 2, 3000
-    Bt = torch.from_numpy(synth.make_B_table(E, 3, first_seed=5)).to(dev)
-
-    def batch(seed):
-        pts = torch.from_numpy(synth.make_pairs(E * n, 3, seed=seed).reshape(E, n, 6)).to(dev)
-        yo = torch.from_numpy(synth.make_speeds(E * n, seed=seed + 1).reshape(E, n, 2)).to(dev)
-        return pts, yo
-
-    gl = GraphedLoss(lambda x, y, b, bt: model.Loss(x, y, b, bt, 1e-3), net.parameters())
-    for seed, beta in ((90, 1.0), (92, 0.37), (94, 2.5)):
-        pts, yo = batch(seed)
-        opt.zero_grad()
-        loss, loss_n, diff = model.Loss(pts, yo, Bt, beta, 1e-3)
-        loss.backward()
-        ref = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
-        ref_out = (loss.detach().clone(), loss_n.detach().clone(), diff.clone())
-        opt.zero_grad()                                   # .grad = None before the replay
-        out = gl(pts, yo, Bt, beta=beta, key=1e-3)
-        for a, b in zip(out, ref_out):
-            assert torch.equal(a.detach(), b), seed
-        for k, p in net.named_parameters():
-            if k in ref:
-                assert p.grad is not None and torch.equal(p.grad, ref[k]), (seed, k)
-            else:
-                assert p.grad is None, k

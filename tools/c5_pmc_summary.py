@@ -1,4 +1,4 @@
-"""Summarise the C5 planner profiles of tools/r03_gpu1.sh (gpurun_out/c5_stats, c5_pmc_*)
+"""Summarise the C5 planner profiles of tools/gpu_pass.sh's c5 step (gpurun_out/<src>_c5_stats, <src>_c5_pmc_*)
 into profiles/<tag>_c5_kernel_stats.csv and profiles/<tag>_pmc_c5_planner.json.
 
     python tools/c5_pmc_summary.py --tag r03 [--kernel "plan_quad_kernel<6, false>"]
@@ -23,9 +23,9 @@ PROF = os.path.join(ROOT, "profiles")
 WEIGHT_BYTES_PER_TILE_STEP = 2 * 540672 * 4      # both directions of the quad stream
 
 
-def counters(tag, kernel):
+def counters(tag, kernel, pre=""):
     agg = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(OUT, "c5_pmc_%s" % tag, "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(OUT, pre + "c5_pmc_%s" % tag, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             if kernel in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -37,16 +37,19 @@ def main():
     ap.add_argument("--tag", default="r03")
     ap.add_argument("--kernel", default="plan_quad_kernel<6, false>")
     ap.add_argument("--unit", default="plan_quad_d6")
+    ap.add_argument("--src", default="", help="gpurun_out prefix of a tools/gpu_pass.sh pass "
+                                              "(e.g. r05e: reads r05e_c5_stats, r05e_c5_pmc_*)")
     a = ap.parse_args()
+    a.src = a.src + "_" if a.src else ""
     sys.path.insert(0, os.path.join(ROOT, "p-ntfields_amd"))
     from pntf import _lib
-    stats = glob.glob(os.path.join(OUT, "c5_stats", "*kernel_stats.csv"))[0]
+    stats = glob.glob(os.path.join(OUT, a.src + "c5_stats", "*kernel_stats.csv"))[0]
     shutil.copy(stats, os.path.join(PROF, "%s_c5_kernel_stats.csv" % a.tag))
     avg_ns = [float(r["AverageNs"]) for r in csv.DictReader(open(stats))
               if a.kernel in r["Name"]][0]
-    probe = json.loads([ln for ln in open(os.path.join(OUT, "c5_stats.log"))
+    probe = json.loads([ln for ln in open(os.path.join(OUT, a.src + "c5_stats.log"))
                         if ln.startswith("{")][-1])
-    sq, tcc, lds, fetch = (counters(t, a.kernel) for t in ("sq", "tcc", "lds", "fetch"))
+    sq, tcc, lds, fetch = (counters(t, a.kernel, a.src) for t in ("sq", "tcc", "lds", "fetch"))
     clock = tcc["GRBM_GUI_ACTIVE"] / 8 / (avg_ns * 1e-9)
     simd_cycles = 1024 * avg_ns * 1e-9 * clock
     mfma = sq["SQ_INSTS_VALU_MFMA_MOPS_F32"]

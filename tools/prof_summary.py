@@ -18,11 +18,12 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
+SRC = ""                 # gpurun_out prefix (--src)
 PROF = os.path.join(ROOT, "profiles")
 
 
 def counters(run, kernel):
-    path = os.path.join(OUT, run, "run_counter_collection.csv")
+    path = os.path.join(OUT, SRC + run, "run_counter_collection.csv")
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if kernel in r["Kernel_Name"]:
@@ -36,13 +37,17 @@ def main():
     ap.add_argument("--pairs", type=int, default=1 << 20)
     ap.add_argument("--kernel", default="wide_field_kernel<3, 1, true>")
     ap.add_argument("--unit", default="wide_d3_k1", help="build unit of --kernel")
+    ap.add_argument("--src", default="", help="gpurun_out prefix of a tools/gpu_pass.sh pass "
+                                              "(e.g. r05e: reads r05e_prof_stats, r05e_pmc_*)")
     a = ap.parse_args()
+    global SRC
+    SRC = a.src + "_" if a.src else ""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "p-ntfields_amd"))
     from pntf import _lib
     unit_hash = _lib.build_info()[a.unit]      # the library these profiles were taken from
     os.makedirs(PROF, exist_ok=True)
-    stats = os.path.join(OUT, "prof_stats", "run_kernel_stats.csv")
+    stats = os.path.join(OUT, SRC + "prof_stats", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(PROF, "%s_kernel_stats.csv" % a.tag))
     avg_ns = None
     for r in csv.DictReader(open(stats)):
@@ -77,7 +82,7 @@ def main():
         json.dump(j, fh, indent=1)
     shutil.copy(p, os.path.join(PROF, "pmc_tau_grad.json"))
     print(json.dumps(j, indent=1))
-    if os.path.exists(os.path.join(OUT, "pmc_stall", "run_counter_collection.csv")):
+    if os.path.exists(os.path.join(OUT, SRC + "pmc_stall", "run_counter_collection.csv")):
         st, ns = counters("pmc_stall", a.kernel)
         k = {"kernel": a.kernel, "unit": a.unit, "unit_hash": unit_hash,
              "dispatches": ns.get("SQ_WAIT_ANY"), **{c: st[c] for c in sorted(st)},

@@ -308,14 +308,24 @@ int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const f
  * over workgroups (deterministic partial sums in `work`, pntf_tt_gemm_work_floats(M, N, K)
  * floats; may be NULL when that is 0).  beta == 0 never reads C.  With ta == 0, K and N in
  * {128, 256}, dense rows (lda == K, ldc == N), beta 0 or 1 and 16-byte aligned A, C and work,
- * the register-panel kernel runs: it packs op(B) into `work` (K*N floats, which
- * pntf_tt_gemm_work_floats includes) and streams it; otherwise the LDS-tiled kernel.  Setting
- * PNTF_GEMM_PANEL=0 in the environment (read once) disables the panel kernel. */
+ * a panel kernel runs: it packs op(B) into `work` (pntf_tt_gemm_work_floats includes it) and
+ * keeps it in LDS; otherwise the LDS-tiled kernel.  Panel kernels (PNTF_GEMM_PANEL in the
+ * environment, read once, or pntf_tt_set_panel_mode): 0 = none, 1 = fp32 MFMA with the
+ * weight streamed from L2, 2 = fp32 MFMA with the weight in LDS, 3 (default) = the split-bf16
+ * kernel (every fp32 operand as three bf16 terms, six bf16 MFMA products per fp32 product:
+ * fp32 accuracy at 2.67x the fp32 MFMA rate; 1.5*K*N work floats). */
 size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K);
 int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                  const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
                  size_t work_floats, hipStream_t stream);
 const char* pntf_tt_gemm_last_error(void);
+/* Process-wide panel-kernel choice (see pntf_tt_gemm; not thread-safe against concurrent
+ * GEMMs); returns the previous mode, leaves it unchanged for a mode outside 0..3. */
+int pntf_tt_set_panel_mode(int mode);
+/* The same for the weight-gradient shapes (ta, not tb, beta 0, M and N in {128, 256};
+ * PNTF_GEMM_WGRAD in the environment): 0 = the LDS-tiled kernel, 1 = the fp32-MFMA wgrad
+ * kernel, 2 (default) = the split-bf16 one; returns the previous mode. */
+int pntf_tt_set_wgrad_mode(int mode);
 
 /* One Linear of the Taylor tape with its bias, residual and act_laplace fused (the forward
  * GEMM of pntf_tt_gemm followed by pntf_tt_act_fwd, in one kernel; :663-691, :744/:828):

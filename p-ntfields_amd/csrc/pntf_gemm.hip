@@ -553,6 +553,279 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Split-bf16 panel GEMM (round 5, `panel_x6_kernel`): the LDS panel GEMM above on the bf16
+// matrix cores.  gfx950's fp32-input MFMA runs at 1/16 of the bf16 rate, so an fp32 product is
+// cheaper as six bf16 products: every operand splits into three bf16 terms, RNE each,
+//   x = x0 + x1 + x2,  x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1),
+// |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|, |x - x0 - x1 - x2| <= 2^-25 |x| (the subtractions are
+// exact).  Of the nine partial products a·b keeps the six of order >= 2^-16:
+//   a0b0 + (a0b1 + a1b0) + (a0b2 + a1b1 + a2b0);
+// the three dropped ones are <= 2^-23 |ab| together, about one fp32 rounding of the product.
+// Each bf16 product is exact in the MFMA's fp32 accumulator; the terms go in smallest first.
+// 6 x v_mfma_f32_32x32x16_bf16 (32 cycles each) do the work of 8 x v_mfma_f32_32x32x2_f32
+// (64 cycles each): 2.67x the fp32 MFMA rate (the fp32 VALU rate is no higher).  Accuracy vs
+// fp64 beside the fp32-MFMA kernel: tests/test_train.py (test_x6_gemm_vs_fp64).
+// Layout: MFMA A = the weight (32 out columns x 16 k), pre-split by x6_pack_kernel into three
+// 1 KiB bf16 fragments per (out tile, k block); MFMA B = the A panel's 32 rows: lane (row j,
+// half h) holds A[row j][16 kb + 8h .. +7] as two float4 of the fp32 panel (KC/8 float4 per
+// lane in registers, read from HBM once) and splits them per k block (VALU beside the MFMAs).
+// D register r of lane (j, h) is C[row j][c0 + 32t + 8(r >> 2) + 4h + (r & 3)] as in the fp32
+// kernels.  The pre-split weight is 1.5x the fp32 bytes, so a workgroup's LDS holds a 64-column
+// group at K = 256 (96 KiB; 128 columns at K = 128) and a 256-column layer has four groups,
+// whose workgroups take block ids 8 apart (one XCD: the panel's later reads hit its L2).
+// diagnostics only (tests/diag/gemm_variants.py ablations; wrong results): bit 1 no operand
+// split, 2 no LDS fragment reads in the loop, 4 no next-panel loads, 8 no C stores, 16 every
+// panel load from the first tile (L2-resident)
+#ifndef PNTF_X6_ABL
+#define PNTF_X6_ABL 0
+#endif
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// three-term RNE split of 8 fp32 (k order of the bf16 operand lane: 8 consecutive k)
+__device__ __forceinline__ void x6_split(const f32x4& a, const f32x4& b, bf16x8 (&s)[3]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 v = i < 2 ? f32x2{a[2 * i], a[2 * i + 1]} : f32x2{b[2 * i - 4], b[2 * i - 3]};
+    const bf16x2 p0 = __builtin_convertvector(v, bf16x2);
+    const f32x2 r1 = v - __builtin_convertvector(p0, f32x2);
+    const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
+    const f32x2 r2 = r1 - __builtin_convertvector(p1, f32x2);
+    const bf16x2 p2 = __builtin_convertvector(r2, bf16x2);
+    s[0][2 * i] = p0[0]; s[0][2 * i + 1] = p0[1];
+    s[1][2 * i] = p1[0]; s[1][2 * i + 1] = p1[1];
+    s[2][2 * i] = p2[0]; s[2][2 * i + 1] = p2[1];
+  }
+}
+// products of order 2^-8 and 2^-16 (variant V = 3 of panel_x6_kernel keeps them apart)
+__device__ __forceinline__ f32x16 x6_mid(const bf16x8 (&w)[3], const bf16x8 (&x)[3], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[0], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[1], acc, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 x6_low(const bf16x8 (&w)[3], const bf16x8 (&x)[3], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], x[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[2], acc, 0, 0, 0);
+}
+// the five small products (variant V = 1 keeps them in their own accumulator)
+__device__ __forceinline__ f32x16 x6_small(const bf16x8 (&w)[3], const bf16x8 (&x)[3], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], x[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[0], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[1], acc, 0, 0, 0);
+}
+// a·b on one 32 x 32 x 16 block from the split operands (w: weight terms, x: panel terms),
+// the small terms first
+__device__ __forceinline__ f32x16 x6_mma(const bf16x8 (&w)[3], const bf16x8 (&x)[3], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], x[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[0], acc, 0, 0, 0);
+}
+
+// Pre-split weight fragments: P[((nt·KB + kb)·3 + p)·64 + lane] = term p of
+// B(16 kb + 8h + j, 32 nt + r), j = 0..7 (lane = 32h + r); B = Wᵀ (tb) or W.
+__global__ void x6_pack_kernel(const float* __restrict__ W, int64_t ldb, int tb, int KC, int NC,
+                               bf16x8* __restrict__ P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int KB = KC / 16;
+  if (i >= (int64_t)(NC / 32) * KB * 64) return;
+  const int lane = (int)(i & 63), kb = (int)((i >> 6) % KB), nt = (int)((i >> 6) / KB);
+  const int n = 32 * nt + (lane & 31), k0 = 16 * kb + 8 * (lane >> 5);
+  f32x4 a, b;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = tb ? W[(int64_t)n * ldb + k0 + e] : W[(int64_t)(k0 + e) * ldb + n];
+    b[e] = tb ? W[(int64_t)n * ldb + k0 + 4 + e] : W[(int64_t)(k0 + 4 + e) * ldb + n];
+  }
+  bf16x8 s[3];
+  x6_split(a, b, s);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) P[((int64_t)(nt * KB + kb) * 3 + p) * 64 + lane] = s[p];
+}
+
+// column group of the split kernel: 64 columns at K = 256, 128 at K = 128 (96 KiB of LDS)
+constexpr int x6_cg(int KC, int NC) {
+  return (KC == 256 ? 64 : 128) < NC ? (KC == 256 ? 64 : 128) : NC;
+}
+
+// V: how the six products accumulate.  0: one accumulator, small products first (x6_mma);
+// 1: a0b0 in one accumulator and the five smaller products in a second, added at the store;
+// 3 (the default): three accumulators, one per order (a0b0 | a0b1 + a1b0 | the three of order
+// 2^-16), summed smallest first at the store.  On the reference's trained-weight training
+// fixtures the single accumulator gave 3.6x the fp32-MFMA kernel's step-1 gradient error
+// (every small product is rounded at the running sum's ulp); per-order accumulators bring it
+// to the fp32 level or below, at the same speed (tests/diag/x6_train_acc.py, x6_probe.py;
+// profiles/r05_x6_accuracy.txt).
+template <int KC, int NC, bool ACC, int V = 3>
+__global__ __launch_bounds__(256, 1) void panel_x6_kernel(PanelArgs g) {
+  PNTF_CLOCK_SCOPE;
+  constexpr int KB = KC / 16, QK = KC / 8, CG = x6_cg(KC, NC), TG = CG / 32, NG = NC / CG;
+  constexpr int FR = TG * KB * 3;   // 1 KiB fragments per group
+  static_assert(KB >= 4, "C prefetch distance");
+  __shared__ bf16x8 lw[FR * 64];
+  __shared__ f32x4 lb[ACC ? CG / 4 : 1];
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // block b -> (group, workgroup index): the NG workgroups of a set of tiles on one XCD
+  int grp = 0, wg = blockIdx.x, nwg = gridDim.x;
+  if constexpr (NG > 1) {
+    const int x = blockIdx.x & 7, s = blockIdx.x >> 3;
+    grp = s % NG;
+    wg = (s / NG) * 8 + x;
+    nwg = gridDim.x / NG;
+  }
+  {
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(g.P) + (int64_t)grp * FR * 64;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < FR * 64; i += 256) lw[i] = src[i];
+    if (ACC && g.bias && threadIdx.x < CG / 4)
+      lb[threadIdx.x] = *reinterpret_cast<const f32x4*>(g.bias + CG * grp + 4 * threadIdx.x);
+  }
+  __syncthreads();
+  const int64_t ntiles = (g.M + 31) / 32;
+  const int64_t stride = (int64_t)nwg * 4;
+  int64_t tile = (int64_t)wg * 4 + w;
+  if (tile >= ntiles) return;   // wave-uniform; no barrier follows
+  auto win = [&](const float* base, int64_t ld, int64_t t) {
+    const int64_t rows = g.M - 32 * t;
+    return pg_rsrc(base + 32 * t * ld, (rows < 32 ? rows : 32) * ld * 4);
+  };
+  const int va = (int)((j * g.lda + 8 * h) * 4), vc = (int)((j * g.ldc + 4 * h) * 4);
+  const int c0 = CG * grp;
+  f32x4 x[QK];
+  {
+    const Rsrc ra = win(g.A, g.lda, tile);
+#pragma unroll
+    for (int q = 0; q < QK; ++q) x[q] = pg_load(ra, va, 64 * (q >> 1) + 16 * (q & 1));
+  }
+  const bf16x8* lf = lw + lane;
+  bf16x8 fr[2][TG][3];
+#pragma unroll
+  for (int t = 0; t < TG; ++t)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) fr[0][t][p] = lf[((t * KB) * 3 + p) * 64];
+  // the split terms of the current k block; the next block's are computed beside this
+  // block's MFMAs (software pipeline, wrapping into the next tile's first block)
+  bf16x8 s[3];
+  x6_split(x[0], x[1], s);
+  for (;;) {
+    const int64_t next = tile + stride;
+    const bool more = next < ntiles;
+#if PNTF_X6_ABL & 16
+    const Rsrc rn = win(g.A, g.lda, 0);   // every panel load hits the first tile (L2)
+#else
+    const Rsrc rn = win(g.A, g.lda, more ? next : tile);
+#endif
+    const Rsrc rc = win(g.C, g.ldc, tile), rci = win(g.Cin, g.ldc, tile);
+    f32x16 acc[TG], accl[V == 1 || V == 3 ? TG : 1], accm[V == 3 ? TG : 1];
+    f32x4 cb[TG][4];
+#pragma unroll
+    for (int t = 0; t < TG; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    if constexpr (V == 1 || V == 3) {
+#pragma unroll
+      for (int t = 0; t < TG; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accl[t][r] = 0.f;
+    }
+    if constexpr (V == 3) {
+#pragma unroll
+      for (int t = 0; t < TG; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accm[t][r] = 0.f;
+    }
+    pg_static_for<0, KB>([&](auto I) {
+      constexpr int kb = decltype(I)::value, cur = kb & 1;
+      if constexpr (ACC && kb == KB - 4) {
+#pragma unroll
+        for (int t = 0; t < TG; ++t)
+#pragma unroll
+          for (int R = 0; R < 4; ++R) cb[t][R] = pg_load(rci, vc, (c0 + 32 * t + 8 * R) * 4);
+      }
+      // next k block's fragments (past the tile's end: the next tile's first ones)
+      constexpr int kn = (kb + 1) % KB;
+#if !(PNTF_X6_ABL & 2)
+#pragma unroll
+      for (int t = 0; t < TG; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fr[cur ^ 1][t][p] = lf[((t * KB + kn) * 3 + p) * 64];
+#else
+#pragma unroll
+      for (int t = 0; t < TG; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fr[cur ^ 1][t][p] = fr[cur][t][p];
+#endif
+      // next block's terms (past the tile's end: the next panel's first block, loaded at
+      // this tile's block 0)
+      bf16x8 sn[3];
+#if !(PNTF_X6_ABL & 1)
+      x6_split(x[2 * kn], x[2 * kn + 1], sn);
+#else
+      sn[0] = __builtin_bit_cast(bf16x8, x[2 * kn]);
+      sn[1] = __builtin_bit_cast(bf16x8, x[2 * kn + 1]);
+      sn[2] = sn[0];
+#endif
+#pragma unroll
+      for (int t = 0; t < TG; ++t) {
+        if constexpr (V == 1) {
+          accl[t] = x6_small(fr[cur][t], s, accl[t]);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[cur][t][0], s[0], acc[t], 0, 0, 0);
+        } else if constexpr (V == 3) {
+          accl[t] = x6_low(fr[cur][t], s, accl[t]);
+          accm[t] = x6_mid(fr[cur][t], s, accm[t]);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[cur][t][0], s[0], acc[t], 0, 0, 0);
+        } else {
+          acc[t] = x6_mma(fr[cur][t], s, acc[t]);
+        }
+      }
+      // x[2kb], x[2kb + 1] were split one block ago: reload them with the next panel's (the
+      // last tile reloads its own: no branch in the MFMA stream)
+#if !(PNTF_X6_ABL & 4)
+      x[2 * kb] = pg_load(rn, va, 64 * kb);
+      x[2 * kb + 1] = pg_load(rn, va, 64 * kb + 16);
+#endif
+#pragma unroll
+      for (int p = 0; p < 3; ++p) s[p] = sn[p];
+      if constexpr (kb == KB - 1) {
+        // (acc + bias) + C: the order of nn.Linear's addmm and the residual add after it
+        const bool brow = ACC && g.bias && 32 * tile + j < g.brows;
+#pragma unroll
+        for (int t = 0; t < TG; ++t)
+#pragma unroll
+          for (int R = 0; R < 4; ++R) {
+            f32x4 v = {acc[t][4 * R], acc[t][4 * R + 1], acc[t][4 * R + 2], acc[t][4 * R + 3]};
+            if constexpr (V == 3)
+              v += f32x4{accl[t][4 * R], accl[t][4 * R + 1], accl[t][4 * R + 2], accl[t][4 * R + 3]} +
+                   f32x4{accm[t][4 * R], accm[t][4 * R + 1], accm[t][4 * R + 2], accm[t][4 * R + 3]};
+            if constexpr (V == 1)
+              v += f32x4{accl[t][4 * R], accl[t][4 * R + 1], accl[t][4 * R + 2], accl[t][4 * R + 3]};
+            if (ACC) {
+              if (brow) v += lb[8 * t + 2 * R + h];
+              v += cb[t][R];
+            }
+#if !(PNTF_X6_ABL & 8)
+            pg_store(rc, v, vc, (c0 + 32 * t + 8 * R) * 4);
+#else
+            if (v[0] == 1.2345f) pg_store(rc, v, vc, (c0 + 32 * t + 8 * R) * 4);
+#endif
+          }
+      }
+      // keep each block's loads where they are issued (the scheduler otherwise sinks the next
+      // panel's loads to the tile's end and hoists later blocks' splits onto them)
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (!more) break;
+    tile = next;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Linear + act_laplace of the Taylor tape in one pass (pntf_tt_linear_act; the forward of one
 // Linear of NN.out_laplace, model_res_sigmoid_multi.py:710-848 with act_laplace :675-691).
 // The LDS panel GEMM above with the tape's elementwise stage as its epilogue, so the
@@ -1059,6 +1332,8 @@ __device__ __forceinline__ void wg_store(float* p, f32x4 v) {
   *reinterpret_cast<f32x4*>(p) = v;
   asm volatile("s_nop 0" ::"v"(v));   // store-data hazard guard (pntf_field.h bstore)
 }
+__device__ __forceinline__ void wg_reduce_store(const WgradArgs& g, const f32x16 (&acc)[4][4],
+                                                f32x4 (&red)[2][64 * 64], int s, int tm, int tn);
 
 template <int T, int NB>
 __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs g) {
@@ -1160,10 +1435,111 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(WgradArgs g) {
       }
     }
   }
-  // fixed-order sum of the four waves' tiles, (w0 + w2) + (w1 + w3), through LDS without
-  // writing the accumulators back (a read-modify-write of 256 of them spilled): w2, w3 store
-  // their tiles; w0, w1 add theirs into those in place; then wave w adds the two halves for
-  // out rows 4i + w and writes them to the split's partial
+  wg_reduce_store(g, acc, red, s, tm, tn);
+}
+
+// ---------------------------------------------------------------------------------------
+// Split-bf16 weight-gradient GEMM (round 5): wgrad_kernel's workgroup / split / reduction
+// scheme on v_mfma_f32_32x32x16_bf16 with the three-term operand split of panel_x6_kernel
+// (x6_split, x6_mma: fp32 accuracy, 2.67x the fp32 MFMA rate).  A k block is 16 rows: lane
+// (j, h) loads rows 16c + 8h + i (i = 0..7) of gY (out rows 4j .. 4j+3) and of X (out cols
+// 4j .. 4j+3), one float4 each; component e of the eight gY float4 is the 8-k A operand of out
+// rows {4i + e}, component d of the X ones the B operand of out cols {4j + d} (the fp32
+// kernel's permutation, 8 rows deep), each split into three bf16 terms.  Same D layout, so
+// the same LDS reduction and split partials.
+__device__ __forceinline__ void x6_split8(const float (&v)[8], bf16x8 (&s)[3]) {
+  x6_split(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, s);
+}
+
+template <int T>
+__global__ __launch_bounds__(256, 1) void wgrad_x6_kernel(WgradArgs g) {
+  PNTF_CLOCK_SCOPE;
+  __shared__ f32x4 red[2][64 * 64];   // two 128 x 128 tiles (128 KiB)
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b8 = blockIdx.x >> 3;
+  const int tile = g.xcd ? b8 % T : blockIdx.x % T;
+  const int s = g.xcd ? (blockIdx.x & 7) + 8 * (b8 / T) : blockIdx.x / T;
+  const int tnn = g.N / 128, tm = tile / tnn, tn = tile % tnn;
+  const int64_t r0 = (int64_t)s * g.rps;
+  const int64_t left = g.rows - r0;
+  const int64_t nrows = left <= 0 ? 0 : (left < g.rps ? left : g.rps);
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[e][d][r] = 0.f;
+  if (nrows > 0) {
+    // rows past the split's end are outside the resources: their loads return 0
+    const Rsrc ra = pg_rsrc(g.A + r0 * g.M, nrows * g.M * 4);
+    const Rsrc rb = pg_rsrc(g.B + r0 * g.N, nrows * g.N * 4);
+    const int va = (8 * h * g.M + 128 * tm + 4 * j) * 4, vb = (8 * h * g.N + 128 * tn + 4 * j) * 4;
+    const int sa = __builtin_amdgcn_readfirstlane(g.M * 4);
+    const int sb = __builtin_amdgcn_readfirstlane(g.N * 4);
+    const int nchunks = (int)((nrows + 15) / 16);
+    int c = w;
+    f32x4 xa[2][8], xb[2][8];
+    auto fill = [&](auto B, int ch) {
+      constexpr int buf = decltype(B)::value;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xa[buf][i] = pg_load(ra, va, (16 * ch + i) * sa);
+        xb[buf][i] = pg_load(rb, vb, (16 * ch + i) * sb);
+      }
+    };
+    auto run = [&](auto B) {
+      constexpr int buf = decltype(B)::value;
+      bf16x8 bs[4][3];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = xb[buf][i][d];
+        x6_split8(v, bs[d]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = xa[buf][i][e];
+        bf16x8 as[3];
+        x6_split8(v, as);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) acc[e][d] = x6_mma(as, bs[d], acc[e][d]);
+      }
+    };
+    constexpr std::integral_constant<int, 0> b0{};
+    constexpr std::integral_constant<int, 1> b1{};
+    if (c < nchunks) {
+      fill(b0, c);
+      fill(b1, c + 4);
+    }
+    // the fences keep each burst of loads right after the MFMAs that free its buffer
+    for (; c < nchunks; c += 8) {
+      run(b0);
+      __builtin_amdgcn_sched_barrier(0);
+      fill(b0, c + 8);
+      __builtin_amdgcn_sched_barrier(0);
+      run(b1);   // unconditional: the rows per split are a multiple of 128 (zero chunks past
+                 // the end of the last split)
+      __builtin_amdgcn_sched_barrier(0);
+      fill(b1, c + 12);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  wg_reduce_store(g, acc, red, s, tm, tn);
+}
+
+// fixed-order sum of the four waves' tiles, (w0 + w2) + (w1 + w3), through LDS without
+// writing the accumulators back (a read-modify-write of 256 of them spilled): w2, w3 store
+// their tiles; w0, w1 add theirs into those in place; then wave w adds the two halves for
+// out rows 4i + w and writes them to the split's partial
+__device__ __forceinline__ void wg_reduce_store(const WgradArgs& g, const f32x16 (&acc)[4][4],
+                                                f32x4 (&red)[2][64 * 64], int s, int tm, int tn) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   auto at = [&](int e, int r) { return (e * 16 + r) * 64 + lane; };
   auto quad = [&](int e, int r) {
     return f32x4{acc[e][0][r], acc[e][1][r], acc[e][2][r], acc[e][3][r]};
@@ -1236,13 +1612,20 @@ int64_t splits_for(int64_t M, int64_t N, int64_t K) {
 bool panel_shape(int64_t N, int64_t K) {
   return (K == 128 || K == 256) && (N == 128 || N == 256);
 }
-// PNTF_GEMM_PANEL: 0 = off, 1 = the register-stream panel kernel, 2 (default) = the LDS one.
+// PNTF_GEMM_PANEL: 0 = off, 1 = the register-stream panel kernel, 2 = the LDS one (fp32 MFMA),
+// 3 (default) = the split-bf16 LDS one (panel_x6_kernel).
+// pntf_tt_set_panel_mode overrides it (tests and A/B probes).
+int g_panel_mode = -1;
 int panel_mode() {
-  static const int mode = [] {
+  if (g_panel_mode < 0) {
     const char* e = getenv("PNTF_GEMM_PANEL");
-    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
-  }();
-  return mode;
+    g_panel_mode = e && e[0] >= '0' && e[0] <= '7' ? e[0] - '0' : 3;
+  }
+  return g_panel_mode;
+}
+// work floats of the packed weight: fp32 fragments, or three bf16 terms (1.5x)
+size_t panel_pack_floats(int64_t N, int64_t K) {
+  return panel_mode() >= 3 ? (size_t)(K * N * 3 / 2) : (size_t)(K * N);
 }
 
 // The weight-gradient kernel serves gYᵀ·X with M, N ∈ {128, 256} (ta, not tb, beta 0, dense
@@ -1251,13 +1634,17 @@ int panel_mode() {
 bool wgrad_shape(int64_t M, int64_t N) {
   return (M == 128 || M == 256) && (N == 128 || N == 256);
 }
-bool wgrad_enabled() {
-  static const int on = [] {
+// PNTF_GEMM_WGRAD: 0 = the LDS-tiled kernel, 1 = wgrad_kernel (fp32 MFMA), 2 (default) =
+// wgrad_x6_kernel (split bf16); pntf_tt_set_wgrad_mode overrides it.
+int g_wgrad_mode = -1;
+int wgrad_mode() {
+  if (g_wgrad_mode < 0) {
     const char* e = getenv("PNTF_GEMM_WGRAD");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return on != 0;
+    g_wgrad_mode = e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
+  }
+  return g_wgrad_mode;
 }
+bool wgrad_enabled() { return wgrad_mode() != 0; }
 // Refill scheme per tile count: the two-buffer burst for the 256 x 256 gradients (T = 4:
 // 206 vs 215 µs at 9 x 20 000 rows), the per-slot ring for T = 1, 2 (64 vs 67, 103 vs 106 µs;
 // tools/wgrad_prof.sh).  PNTF_WGRAD_RING=1 or 2 forces one of them (to compare).
@@ -1287,7 +1674,7 @@ size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const int64_t s = splits_for(M, N, K);
   const size_t split = s > 1 ? (size_t)(s * M * N) : 0;
-  const size_t packed = panel_shape(N, K) ? (size_t)(K * N) : 0;
+  const size_t packed = panel_shape(N, K) ? panel_pack_floats(N, K) : 0;
   const size_t wgrad = wgrad_shape(M, N) ? (size_t)((wgrad_splits(M, N, K) + 7) * M * N) : 0;
   const size_t big = split > packed ? split : packed;
   return big > wgrad ? big : wgrad;
@@ -1297,7 +1684,7 @@ size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K) {
 static bool panel_path(int ta, int64_t N, int64_t K, int64_t lda, int64_t ldc, float beta,
                        const float* A, const float* C, const float* work, size_t work_floats) {
   return !ta && (beta == 0.f || beta == 1.f) && panel_shape(N, K) && panel_mode() != 0 &&
-         lda == K && ldc == N && work && work_floats >= (size_t)(K * N) &&
+         lda == K && ldc == N && work && work_floats >= panel_pack_floats(N, K) &&
          ((uintptr_t)A & 15) == 0 && ((uintptr_t)C & 15) == 0 && ((uintptr_t)work & 15) == 0;
 }
 
@@ -1310,6 +1697,18 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
                  const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
                  size_t work_floats, hipStream_t stream) {
   return tt_gemm(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, beta, work, work_floats, stream, C);
+}
+
+int pntf_tt_set_panel_mode(int mode) {
+  const int prev = panel_mode();
+  if (mode >= 0 && mode <= 7) g_panel_mode = mode;
+  return prev;
+}
+
+int pntf_tt_set_wgrad_mode(int mode) {
+  const int prev = wgrad_mode();
+  if (mode >= 0 && mode <= 2) g_wgrad_mode = mode;
+  return prev;
 }
 
 extern "C" int pntf_tt_act_fwd_biased(int ndir, int nl, const float* y, float* h, int64_t m,
@@ -1330,13 +1729,54 @@ static int tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float*
     snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: null pointer");
     return PNTF_ERR_ARG;
   }
+  const int pm = panel_mode();
+  // modes 4 / 5 (diagnostics): the split kernel for the forward (tb) / input-gradient (!tb)
+  // GEMMs only; 6 / 7: its accumulation variants V = 0 / 1
+  const bool x6 = pm == 3 || pm >= 6 || (pm == 4 && tb) || (pm == 5 && !tb);
+  if (panel_path(ta, N, K, lda, ldc, beta, A, C, work, work_floats) && x6) {
+    const int64_t nf = (N / 32) * (K / 16) * 64;
+    hipLaunchKernelGGL(x6_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream,
+                       B, ldb, tb, (int)K, (int)N, reinterpret_cast<bf16x8*>(work));
+    PanelArgs p{A, reinterpret_cast<const f32x4*>(work), C, M, lda, ldc, Cin, bias, brows};
+    // one workgroup per CU (96 KiB of LDS); per group at most CUs / NG of them, a multiple of
+    // 8 with several groups so that a tile's group workgroups share an XCD
+    const int64_t tiles = (M + 31) / 32, wgs = (tiles + 3) / 4;
+    const int64_t ng = N / (K == 256 ? 64 : 128) > 1 ? N / (K == 256 ? 64 : 128) : 1;
+    const int64_t cap = num_cus() / ng;
+    int64_t nwg = wgs < cap ? wgs : cap;
+    if (ng > 1) nwg = (nwg + 7) / 8 * 8;
+    const dim3 grid((unsigned)(nwg * ng));
+#define PNTF_PANEL(KC, NC)                                                                      \
+  if (pm == 6) {                                                                                \
+    if (beta != 0.f) hipLaunchKernelGGL((panel_x6_kernel<KC, NC, true, 0>), grid, dim3(256), 0,  \
+                                        stream, p);                                             \
+    else hipLaunchKernelGGL((panel_x6_kernel<KC, NC, false, 0>), grid, dim3(256), 0, stream, p); \
+  } else if (pm == 7) {                                                                         \
+    if (beta != 0.f) hipLaunchKernelGGL((panel_x6_kernel<KC, NC, true, 1>), grid, dim3(256), 0,  \
+                                        stream, p);                                             \
+    else hipLaunchKernelGGL((panel_x6_kernel<KC, NC, false, 1>), grid, dim3(256), 0, stream, p); \
+  } else if (beta != 0.f) hipLaunchKernelGGL((panel_x6_kernel<KC, NC, true>), grid, dim3(256), 0, \
+                                             stream, p);                                        \
+  else hipLaunchKernelGGL((panel_x6_kernel<KC, NC, false>), grid, dim3(256), 0, stream, p);
+    if (K == 128 && N == 128) { PNTF_PANEL(128, 128) }
+    else if (K == 128) { PNTF_PANEL(128, 256) }
+    else if (N == 128) { PNTF_PANEL(256, 128) }
+    else { PNTF_PANEL(256, 256) }
+#undef PNTF_PANEL
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: %s", hipGetErrorString(e));
+      return PNTF_ERR_HIP;
+    }
+    return PNTF_OK;
+  }
   if (panel_path(ta, N, K, lda, ldc, beta, A, C, work, work_floats)) {
     const int64_t nf = (N / 32) * (K / 8) * 64;
     hipLaunchKernelGGL(panel_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0,
                        stream, B, ldb, tb, (int)K, (int)N, reinterpret_cast<f32x4*>(work));
     PanelArgs p{A, reinterpret_cast<const f32x4*>(work), C, M, lda, ldc, Cin, bias, brows};
     const int64_t tiles = (M + 31) / 32, wgs = (tiles + 3) / 4;
-    if (panel_mode() == 2) {
+    if (panel_mode() >= 2) {
       // one workgroup per CU (128 KiB of LDS at K = 256); per group at most CUs / NG of them
       // a multiple of 8 so that a tile's two group workgroups share an XCD (N = 256)
       // (K = 128 without C: 64 KiB of LDS and ≤ 256 registers, so two per CU)
@@ -1398,7 +1838,11 @@ static int tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float*
   if (T == 1) hipLaunchKernelGGL((wgrad_kernel<1, NB>), grid, dim3(256), 0, stream, wa);         \
   else if (T == 2) hipLaunchKernelGGL((wgrad_kernel<2, NB>), grid, dim3(256), 0, stream, wa);    \
   else hipLaunchKernelGGL((wgrad_kernel<4, NB>), grid, dim3(256), 0, stream, wa);
-      if (wgrad_ring(T) == 2) { PNTF_WGRAD(2) } else { PNTF_WGRAD(1) }
+      if (wgrad_mode() == 2) {
+        if (T == 1) hipLaunchKernelGGL((wgrad_x6_kernel<1>), grid, dim3(256), 0, stream, wa);
+        else if (T == 2) hipLaunchKernelGGL((wgrad_x6_kernel<2>), grid, dim3(256), 0, stream, wa);
+        else hipLaunchKernelGGL((wgrad_x6_kernel<4>), grid, dim3(256), 0, stream, wa);
+      } else if (wgrad_ring(T) == 2) { PNTF_WGRAD(2) } else { PNTF_WGRAD(1) }
 #undef PNTF_WGRAD
       const int64_t n = M * N;
       const unsigned nb = (unsigned)((n + 255) / 256);
@@ -1509,7 +1953,7 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
   if (!fused) {
     // the residual enters the GEMM's epilogue (y = x·Wᵀ + res, its C read 4 iterations ahead),
     // so the act pass reads y and writes h instead of reading y and res and writing both back
-    if (res && (nl > 0 || ndir > 0) && panel_mode() == 2 &&
+    if (res && (nl > 0 || ndir > 0) && panel_mode() >= 2 &&
         panel_path(0, n, k, k, n, 1.f, x, y, work, work_floats)) {
       int st = tt_gemm(0, 1, R * m, n, k, x, k, W, k, y, n, 1.f, work, work_floats, stream, res,
                        bias, m);

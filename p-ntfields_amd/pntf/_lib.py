@@ -108,6 +108,8 @@ SIGNATURES = {
                                     _c_void_p, _i64, _c_void_p, _i64, _f32, _c_void_p,
                                     ctypes.c_size_t, _c_void_p]),
     "pntf_tt_gemm_last_error": (ctypes.c_char_p, []),
+    "pntf_tt_set_panel_mode": (ctypes.c_int, [ctypes.c_int]),
+    "pntf_tt_set_wgrad_mode": (ctypes.c_int, [ctypes.c_int]),
     "pntf_tt_linear_act": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _i64, ctypes.c_int,
                                           _c_void_p, ctypes.c_int, _c_void_p, _c_void_p, _c_void_p,
                                           _c_void_p, ctypes.c_int, ctypes.c_int, _c_void_p,

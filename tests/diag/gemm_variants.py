@@ -21,7 +21,7 @@ def timeit(fn, reps=10):
     return a.elapsed_time(b) / reps
 
 
-def main(names, pairs=20000):
+def main(names, pairs=20000, check=True):
     dev = torch.device("cuda:0")
     V = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)   # noqa: E731
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -54,16 +54,18 @@ def main(names, pairs=20000):
             ref = X @ W.t()
             f()
             torch.cuda.synchronize()
-            assert (Y - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
+            assert not check or (Y - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
             f = run(GX, G, W, 0, 0, rows, K, N)
             res[tag + "_bwdx"] = round(fl / timeit(f), 1)
             ref = G @ W
             f()
             torch.cuda.synchronize()
-            assert (GX - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
+            assert not check or (GX - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
             res[tag + "_bwdw"] = round(fl / timeit(run(GW, G, X, 1, 0, N, K, rows)), 1)
         print(name, res, flush=True)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    # names starting with "abl" are ablation builds (wrong results: no check)
+    for nm in sys.argv[1:]:
+        main([nm], check=not nm.startswith("abl"))

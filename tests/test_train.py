@@ -140,20 +140,70 @@ def test_loss_backward_vs_reference(name, dim):
             assert p.grad is None, k            # encoder1.0: never used, no gradient
 
 
+_F64_TRAJ = {}
+
+
+def _f64_two_steps(name):
+    """The reference's two training steps in exact arithmetic (fp64 oracle gradients + AdamW,
+    oracle.eikonal_loss_grad / adamw_step): (step-1 gradients, loss after step 1 (the fixture's
+    loss2), parameters after step 2).  Adjudicates the two-step comparison where the
+    reference's own fp32 rounding and ours differ (Adam's first step is lr·sign(g))."""
+    if name not in _F64_TRAJ:
+        dim = 3 if name.endswith("d3.npz") else 6
+        W = _case_weights(name)
+        f, c = _golden_case(name)
+        B = c["B"][0] if c["env"] is None else c["B"]
+        P = {k: v.astype(np.float64).copy() for k, v in W.items()}
+        m = {k: np.zeros_like(v) for k, v in P.items()}
+        v = {k: np.zeros_like(x) for k, x in P.items()}
+        beta = float(f["beta"])
+        g1 = loss2 = None
+        for step in (1, 2):
+            diff, g = O.eikonal_loss_grad(P, c["xp"], c["yobs"], B, c["env"], dim,
+                                          float(f["gamma"]), c["scale"], c["arm"])
+            if step == 1:
+                g1 = g
+            elif c["arm"]:
+                loss2 = beta * float(np.sum(diff)) / diff.size
+            else:
+                E = int(c["env"].max()) + 1
+                loss2 = beta * O.loss_n(diff, f["B_table"], E, diff.size // E)
+            for k in g:
+                O.adamw_step(P[k], g[k], m[k], v[k], step)
+        _F64_TRAJ[name] = (g1, loss2, P)
+    return _F64_TRAJ[name]
+
+
+def test_f64_trajectory_brackets_reference():
+    """The fp64 two-step trajectory the GPU test adjudicates with reproduces the reference's
+    recorded loss after one AdamW step to fp32 rounding (|Δ| <= 6e-7 on all four fixtures)."""
+    for name, _ in CASES:
+        _, loss2, _ = _f64_two_steps(name)
+        assert abs(loss2 - float(load(name)["loss2"])) < 1e-6, name
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,dim", CASES)
 def test_two_adamw_steps_vs_reference(name, dim):
+    """Two Model.train inner steps from the fixture's state against the reference's recorded
+    loss and parameters.  Adam's first update is lr·sign(g), so a weight whose gradient is
+    resolved differently by two fp32 computations (the reference's CPU GEMMs, our split-bf16
+    MFMA ones) moves differently; each check therefore passes against the reference's fp32
+    values or against the exact (fp64) trajectory, with the same bound."""
     from pntf.train import AdamW
     dev = torch.device("cuda:0")
     W = _case_weights(name)
     f = load(name)
+    g64, loss2_64, after64 = _f64_two_steps(name)
     model, net = _nets(dim, W, dev, f["B"] if dim == 6 else None)
     opt = AdamW(net.parameters(), lr=1e-3, weight_decay=0.1)
     grads = []
     for step in range(2):
         loss, loss_n, _ = _loss(model, f, dim, dev)
         if step == 1:
-            assert abs(loss.item() - float(f["loss2"])) < 1e-5 * max(1.0, float(f["loss2"]))
+            tol = 1e-5 * max(1.0, float(f["loss2"]))
+            assert min(abs(loss.item() - float(f["loss2"])), abs(loss.item() - loss2_64)) < tol, \
+                (loss.item(), float(f["loss2"]), loss2_64)
         loss.backward()
         grads.append({k: p.grad.detach().cpu().numpy().copy()
                       for k, p in net.named_parameters() if p.grad is not None})
@@ -177,12 +227,20 @@ def test_two_adamw_steps_vs_reference(name, dim):
             if name not in grads[0]:                 # encoder1.0: no gradient, unchanged
                 assert np.array_equal(got, f[k]), name
                 continue
-            err = np.abs(got - f[k])
-            delta = 2 * max(float(np.abs(grads[0][name] - f["grad:" + name]).max()), 1e-12)
+            # against the reference (δ: our step-1 gradient error vs its gradient) or against
+            # the fp64 trajectory (δ vs the exact gradient), elementwise the closer of the two
             g = np.minimum(np.abs(grads[0][name]), np.abs(grads[1][name]))
-            bound = 2e-6 + 8 * lr * delta / np.maximum(g, delta)
-            worst = np.argmax(err - bound)
-            assert (err <= bound).all(), (name, float(err.flat[worst]), float(bound.flat[worst]))
+            ok = np.zeros(got.shape, bool)
+            worst = None
+            for target, gref in ((f[k], f["grad:" + name]), (after64[name], g64[name])):
+                err = np.abs(got - target)
+                delta = 2 * max(float(np.abs(grads[0][name] - gref).max()), 1e-12)
+                bound = 2e-6 + 8 * lr * delta / np.maximum(g, delta)
+                ok |= err <= bound
+                if worst is None:
+                    i = np.argmax(err - bound)
+                    worst = (float(err.flat[i]), float(bound.flat[i]))
+            assert ok.all(), (name, int((~ok).sum()), worst)
     assert np.array_equal(sd["encoder1.0.weight"].detach().cpu().numpy(), W["encoder1.0.weight"])
 
 
@@ -450,6 +508,51 @@ def test_mfma_gemm_vs_fp64(ta, tb, M, N, K, beta):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tb,M,N,K,beta", [
+    (True, 40001, 256, 256, 0.0),    # forward X·Wᵀ, generator (4 column groups)
+    (True, 129, 128, 256, 0.0),      # forward, generator[3] shape, ragged rows
+    (True, 20003, 256, 128, 0.0),    # forward, encoder[-1] -> generator width
+    (False, 70007, 128, 256, 1.0),   # input gradient gY·W + residual branch
+    (False, 3001, 128, 128, 1.0),    # encoder input gradient (one column group)
+    (False, 1, 256, 128, 0.0),
+])
+def test_x6_gemm_vs_fp64(tb, M, N, K, beta):
+    """The split-bf16 panel kernel (panel_x6_kernel: every fp32 operand as three bf16 terms,
+    six bf16 MFMA products per fp32 product) against an fp64 matmul of the same fp32 operands,
+    beside the fp32-MFMA LDS panel kernel on the same call: elementwise within the fp32
+    accumulation bound 1e-5·sqrt(K)·(|A|·|B|), and its error statistics no worse than fp32's
+    (mean relative error within 1.5x, max within 2x)."""
+    import ctypes
+    from pntf import _lib, train
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + 11)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    ref = A.double() @ (B.double().t() if tb else B.double()) + beta * C0.double()
+    scale = A.double().abs() @ (B.double().abs().t() if tb else B.double().abs()) + 1e-30
+    Ad, Bd = A.to(dev), B.to(dev)
+    rel = {}
+    prev = lib.pntf_tt_set_panel_mode(3)
+    try:
+        for mode in (2, 3):
+            lib.pntf_tt_set_panel_mode(mode)
+            C = C0.to(dev)
+            train.gemm(C, Ad, Bd, False, tb, beta)
+            err = (C.cpu().double() - ref).abs()
+            assert torch.all(err <= 1e-5 * np.sqrt(K) * scale + 1e-6), (mode, float((err / scale).max()))
+            rel[mode] = err / scale
+    finally:
+        lib.pntf_tt_set_panel_mode(prev)
+    m2, m3 = float(rel[2].mean()), float(rel[3].mean())
+    x2, x3 = float(rel[2].max()), float(rel[3].max())
+    print("x6 gemm %s M=%d N=%d K=%d: mean rel err fp32 %.3g x6 %.3g, max %.3g / %.3g"
+          % ("fwd" if tb else "bwd", M, N, K, m2, m3, x2, x3))
+    assert m3 <= 1.5 * m2 + 1e-12 and x3 <= 2.0 * x2 + 1e-12
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fused", [1, 3])
 @pytest.mark.parametrize("dim", [3, 6])
 @pytest.mark.parametrize("n", [1, 77, 333])
@@ -484,9 +587,23 @@ def test_fused_linear_act_ragged_vs_two_kernel(fused, dim, n, monkeypatch):
     d2, g2, t2, v2 = out[2]
     assert torch.allclose(d1, d2, rtol=1e-5, atol=1e-5)
     assert torch.allclose(t1, t2, rtol=1e-6, atol=1e-7)
+    # the fused kernels run fp32 MFMA GEMMs, the pair the split-bf16 ones: where a gradient's
+    # two roundings differ beyond 1e-5 both must be within 1e-4 of the fp64 oracle
+    N = lambda t: t.detach().cpu().numpy()   # noqa: E731
+    ref64 = {}
+
+    def oracle():
+        if not ref64:
+            X = [N(t) for t in (xp, yobs, Bt, env)]
+            ref64["g"] = O.eikonal_loss_grad(W, X[0], X[1], X[2], X[3], dim, 1e-3, 1.0 / n,
+                                             dim == 6)[1]
+            ref64["v"] = O.taylor_vjp(W, X[0], X[2], X[3], dim, g_tau=N(gtau))[1]
+        return ref64
     for k in params:
-        assert _rel(g1[k].detach().cpu().numpy(), g2[k].detach().cpu().numpy()) < 1e-5, k
-        assert _rel(v1[k].detach().cpu().numpy(), v2[k].detach().cpu().numpy()) < 1e-5, k
+        for a, b, w in ((g1, g2, "g"), (v1, v2, "v")):
+            if _rel(N(a[k]), N(b[k])) >= 1e-5:
+                r = oracle()[w][k]
+                assert _rel(N(a[k]), r) < 1e-4 and _rel(N(b[k]), r) < 1e-4, (w, k)
 
 
 @pytest.mark.gpu
@@ -532,8 +649,17 @@ def test_fused_linear_act_matches_two_kernel_path(name, dim, monkeypatch):
     d0, g0 = out[False]
     assert torch.allclose(d1, d0, rtol=1e-5, atol=1e-6)
     assert len(g1) == len(g0)
-    for a, b in zip(g1, g0):
-        assert float((a - b).norm() / b.norm().clamp_min(1e-30)) < 1e-5
+    # fp32-MFMA fused kernels vs the split-bf16 GEMM pair: where the two roundings differ
+    # beyond 1e-5 (in norm) both must be within 1e-4 of the fp64 oracle's gradient
+    keys = [k for k, p in net.named_parameters() if p.grad is not None]
+    g64 = None
+    for k, a, b in zip(keys, g1, g0):
+        if float((a - b).norm() / b.norm().clamp_min(1e-30)) >= 1e-5:
+            if g64 is None:
+                g64 = _f64_two_steps(name)[0]
+            r = torch.from_numpy(g64[k])
+            for t in (a, b):
+                assert float((t.cpu().double() - r).norm() / r.norm()) < 1e-4, k
 
 
 @pytest.mark.gpu
@@ -570,13 +696,15 @@ def test_training_uses_no_vendor_gemm():
         loss.backward()
         torch.cuda.synchronize()
     names = [e.key for e in prof.key_averages()]
-    # weight gradients on the register-streamed wgrad kernel (PNTF_GEMM_WGRAD=0: the LDS-tiled
-    # split-K gemm_kernel)
-    wg = "gemm_kernel" if os.environ.get("PNTF_GEMM_WGRAD") == "0" else "wgrad_kernel"
+    # weight gradients on the split-bf16 register-streamed wgrad kernel (PNTF_GEMM_WGRAD=1: the
+    # fp32-MFMA one, 0: the LDS-tiled split-K gemm_kernel)
+    wg = {"0": "gemm_kernel", "1": "wgrad_kernel"}.get(os.environ.get("PNTF_GEMM_WGRAD", ""),
+                                                       "wgrad_x6_kernel")
     assert any(wg in n for n in names), names
-    # forward / input-gradient Linears run on the LDS panel kernel (PNTF_GEMM_PANEL=1: the
-    # register-stream one)
-    panel = "panel_gemm_kernel" if os.environ.get("PNTF_GEMM_PANEL") == "1" else "panel_lds_kernel"
+    # forward / input-gradient Linears run on the split-bf16 panel kernel (PNTF_GEMM_PANEL=1 /
+    # 2: the fp32-MFMA register-stream / LDS ones)
+    panel = {"1": "panel_gemm_kernel", "2": "panel_lds_kernel"}.get(
+        os.environ.get("PNTF_GEMM_PANEL", ""), "panel_x6_kernel")
     assert any(panel in n for n in names), names
     assert not any("Cijk" in n or "hipblaslt" in n.lower() for n in names), names
 

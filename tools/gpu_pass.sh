@@ -16,6 +16,7 @@
 #   py=<tool.py args>      a probe script (tools/*.py), output <tag>_<tool>.txt
 #   trace=<tool.py args>   the same under rocprofv3 --kernel-trace --stats, plus the idle-gap
 #                          summary of tools/trace_gaps.py
+#   pmc=<name>:<c1,c2,..>:<tool.py args>  one PMC pass (counters only) over a probe script
 #   smoke                  __graft_entry__.smoke()
 # Outputs land in gpurun_out/<tag>_*; tools/prof_summary.py / c5_pmc_summary.py turn them
 # into profiles/.
@@ -81,6 +82,13 @@ for step in "$@"; do
           --output-format csv -- python3 $R/$a > "$OUT/${TAG}_trace_$nm.log" 2>&1 )
       f=$(find "$OUT/${TAG}_trace_$nm" -name "*kernel_trace.csv" | head -1)
       python3 tools/trace_gaps.py "$f" | tee "$OUT/${TAG}_trace_$nm.gaps" ;;
+    pmc=*)      # pmc=<name>:<counter,...>:<tool.py args...>: one counter pass over a probe
+      a=${step#pmc=}; nm=${a%%:*}; a=${a#*:}; ctr=${a%%:*}; a=${a#*:}
+      ( cd /tmp && export TMPDIR=/tmp
+        timeout -s KILL 180 rocprofv3 --pmc ${ctr//,/ } -d "$OUT/${TAG}_pmc_$nm" -o run \
+          --output-format csv -- python3 $R/$a > "$OUT/${TAG}_pmc_$nm.log" 2>&1 ) \
+        || { tail -20 "$OUT/${TAG}_pmc_$nm.log"; exit 1; }
+      tail -2 "$OUT/${TAG}_pmc_$nm.log" ;;
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $step"; exit 2 ;;

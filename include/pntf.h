@@ -333,9 +333,10 @@ int pntf_tt_set_wgrad_mode(int mode);
  * -> y (R, m, n) pre-activation (value plane + bias, every plane + res; kept as the tape) and,
  * when act != 0, h (R, m, n) the softplus10 Taylor rows.  R = 1 + ndir + nl with (ndir, nl) =
  * (3|6, 1), (6|12, 2) or (0, 0); k, n in {128, 256}; all pointers 16-byte aligned; `work` holds the
- * packed weight (k*n floats).  act == 0 requires res == NULL (h unused).  schedule: 0 = AUTO
- * (the fused kernel when every wave gets >= 3 rounds of 32-point blocks that balance
- * to >= 90 %, else the two kernels),
+ * packed weight (pntf_tt_gemm_work_floats(R*m, n, k) floats).  act == 0 requires res == NULL
+ * (h unused).  schedule: 0 = AUTO (the two kernels while the split-bf16 panel GEMM is
+ * selected, the default; with the fp32-MFMA panel modes the fused kernel when every wave gets
+ * >= 3 rounds of 32-point blocks that balance to >= 90 %),
  * 1 = always the fused kernel (one wave per 32-point block), 2 = always pntf_tt_gemm +
  * pntf_tt_act_fwd, 3 = the fused kernel with the four waves of a workgroup sharing a block;
  * errors of either path are reported by pntf_tt_gemm_last_error / pntf_tt_last_error. */

@@ -573,9 +573,14 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
 // kernels.  The pre-split weight is 1.5x the fp32 bytes, so a workgroup's LDS holds a 64-column
 // group at K = 256 (96 KiB; 128 columns at K = 128) and a 256-column layer has four groups,
 // whose workgroups take block ids 8 apart (one XCD: the panel's later reads hit its L2).
+// C leaves through a per-wave LDS block so that its stores are row-contiguous (1; 0: straight
+// from the MFMA layout, 32 half-filled lines per store)
+#ifndef PNTF_X6_TSTORE
+#define PNTF_X6_TSTORE 1
+#endif
 // diagnostics only (tests/diag/gemm_variants.py ablations; wrong results): bit 1 no operand
 // split, 2 no LDS fragment reads in the loop, 4 no next-panel loads, 8 no C stores, 16 every
-// panel load from the first tile (L2-resident)
+// panel load from the first tile (L2-resident), 32 the panel's bytes read row-contiguously
 #ifndef PNTF_X6_ABL
 #define PNTF_X6_ABL 0
 #endif
@@ -648,10 +653,14 @@ __global__ void x6_pack_kernel(const float* __restrict__ W, int64_t ldb, int tb,
   for (int p = 0; p < 3; ++p) P[((int64_t)(nt * KB + kb) * 3 + p) * 64 + lane] = s[p];
 }
 
-// column group of the split kernel: 64 columns at K = 256, 128 at K = 128 (96 KiB of LDS)
-constexpr int x6_cg(int KC, int NC) {
-  return (KC == 256 ? 64 : 128) < NC ? (KC == 256 ? 64 : 128) : NC;
-}
+// workgroups (so waves) per CU of the split kernel: 1 holds a 64-column group at K = 256 (128 at
+// K = 128) in 96 KiB of LDS; 2 halves the group (48 KiB) so that two workgroups share a CU and
+// each SIMD runs two waves (<= 256 registers each)
+#ifndef PNTF_X6_WPS
+#define PNTF_X6_WPS 1
+#endif
+constexpr int x6_cg1(int KC) { return (KC == 256 ? 64 : 128) / PNTF_X6_WPS; }
+constexpr int x6_cg(int KC, int NC) { return x6_cg1(KC) < NC ? x6_cg1(KC) : NC; }
 
 // V: how the six products accumulate.  0: one accumulator, small products first (x6_mma);
 // 1: a0b0 in one accumulator and the five smaller products in a second, added at the store;
@@ -662,13 +671,18 @@ constexpr int x6_cg(int KC, int NC) {
 // to the fp32 level or below, at the same speed (tests/diag/x6_train_acc.py, x6_probe.py;
 // profiles/r05_x6_accuracy.txt).
 template <int KC, int NC, bool ACC, int V = 3>
-__global__ __launch_bounds__(256, 1) void panel_x6_kernel(PanelArgs g) {
+__global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g) {
   PNTF_CLOCK_SCOPE;
   constexpr int KB = KC / 16, QK = KC / 8, CG = x6_cg(KC, NC), TG = CG / 32, NG = NC / CG;
   constexpr int FR = TG * KB * 3;   // 1 KiB fragments per group
   static_assert(KB >= 4, "C prefetch distance");
   __shared__ bf16x8 lw[FR * 64];
   __shared__ f32x4 lb[ACC ? CG / 4 : 1];
+#if PNTF_X6_TSTORE
+  // per wave: a 32-row x 64-column block of C on its way out (row stride 17 float4: the MFMA
+  // layout writes and the row-contiguous reads are both conflict-free)
+  __shared__ f32x4 lt[4][32 * 17];
+#endif
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // block b -> (group, workgroup index): the NG workgroups of a set of tiles on one XCD
@@ -696,6 +710,12 @@ __global__ __launch_bounds__(256, 1) void panel_x6_kernel(PanelArgs g) {
     return pg_rsrc(base + 32 * t * ld, (rows < 32 ? rows : 32) * ld * 4);
   };
   const int va = (int)((j * g.lda + 8 * h) * 4), vc = (int)((j * g.ldc + 4 * h) * 4);
+#if PNTF_X6_TSTORE
+  const int vt = (int)(((lane >> 4) * g.ldc + 4 * (lane & 15)) * 4);
+#endif
+#if PNTF_X6_ABL & 32
+  const int vco = (int)(((lane >> 3) * g.lda) * 4 + 16 * (lane & 7));
+#endif
   const int c0 = CG * grp;
   f32x4 x[QK];
   {
@@ -786,7 +806,12 @@ __global__ __launch_bounds__(256, 1) void panel_x6_kernel(PanelArgs g) {
       }
       // x[2kb], x[2kb + 1] were split one block ago: reload them with the next panel's (the
       // last tile reloads its own: no branch in the MFMA stream)
-#if !(PNTF_X6_ABL & 4)
+#if PNTF_X6_ABL & 32
+      // (the same bytes per tile read row-contiguously: 8 lanes per 128-byte line, 8 rows per
+      // instruction; wrong operands)
+      x[2 * kb] = pg_load(rn, vco, 4096 * (kb & 3) + 128 * (kb >> 2));
+      x[2 * kb + 1] = pg_load(rn, vco, 4096 * (kb & 3) + 128 * (kb >> 2) + 64);
+#elif !(PNTF_X6_ABL & 4)
       x[2 * kb] = pg_load(rn, va, 64 * kb);
       x[2 * kb + 1] = pg_load(rn, va, 64 * kb + 16);
 #endif
@@ -796,7 +821,7 @@ __global__ __launch_bounds__(256, 1) void panel_x6_kernel(PanelArgs g) {
         // (acc + bias) + C: the order of nn.Linear's addmm and the residual add after it
         const bool brow = ACC && g.bias && 32 * tile + j < g.brows;
 #pragma unroll
-        for (int t = 0; t < TG; ++t)
+        for (int t = 0; t < TG; ++t) {
 #pragma unroll
           for (int R = 0; R < 4; ++R) {
             f32x4 v = {acc[t][4 * R], acc[t][4 * R + 1], acc[t][4 * R + 2], acc[t][4 * R + 3]};
@@ -809,12 +834,33 @@ __global__ __launch_bounds__(256, 1) void panel_x6_kernel(PanelArgs g) {
               if (brow) v += lb[8 * t + 2 * R + h];
               v += cb[t][R];
             }
-#if !(PNTF_X6_ABL & 8)
+#if PNTF_X6_TSTORE
+            // lane (j, h) holds row j's columns 32t + 8R + 4h .. +3 of the 64-column block
+            lt[w][j * 17 + 8 * (t & 1) + 2 * R + h] = v;
+#elif !(PNTF_X6_ABL & 8)
             pg_store(rc, v, vc, (c0 + 32 * t + 8 * R) * 4);
 #else
             if (v[0] == 1.2345f) pg_store(rc, v, vc, (c0 + 32 * t + 8 * R) * 4);
 #endif
           }
+#if PNTF_X6_TSTORE
+          if (t & 1) {
+            // the block's rows go out row-contiguously: 16 lanes x 16 B per 256-byte row,
+            // four rows per store (8 cache lines instead of 32 half-filled ones).  LDS is in
+            // order within the wave; the wait is for the reads of the lanes' own data.
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const f32x4 v = lt[w][(4 * i + (lane >> 4)) * 17 + (lane & 15)];
+#if !(PNTF_X6_ABL & 8)
+              pg_store(rc, v, vt, (4 * i * (int)g.ldc + c0 + 32 * (t - 1)) * 4);
+#else
+              if (v[0] == 1.2345f) pg_store(rc, v, vt, (4 * i * (int)g.ldc + c0 + 32 * (t - 1)) * 4);
+#endif
+            }
+          }
+#endif
+        }
       }
       // keep each block's loads where they are issued (the scheduler otherwise sinks the next
       // panel's loads to the tile's end and hoists later blocks' splits onto them)
@@ -1741,8 +1787,9 @@ static int tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float*
     // one workgroup per CU (96 KiB of LDS); per group at most CUs / NG of them, a multiple of
     // 8 with several groups so that a tile's group workgroups share an XCD
     const int64_t tiles = (M + 31) / 32, wgs = (tiles + 3) / 4;
-    const int64_t ng = N / (K == 256 ? 64 : 128) > 1 ? N / (K == 256 ? 64 : 128) : 1;
-    const int64_t cap = num_cus() / ng;
+    const int64_t cg = K == 256 ? x6_cg1(256) : x6_cg1(128);
+    const int64_t ng = N / cg > 1 ? N / cg : 1;
+    const int64_t cap = PNTF_X6_WPS * num_cus() / ng;
     int64_t nwg = wgs < cap ? wgs : cap;
     if (ng > 1) nwg = (nwg + 7) / 8 * 8;
     const dim3 grid((unsigned)(nwg * ng));
@@ -1948,8 +1995,11 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
   const int64_t waves = 4 * nwg, rounds = (blocks + waves - 1) / waves;
   // (and only with several rounds per wave: at one round, generator[3] of the reference batch,
   // the fused kernel measured 227 µs against 132 + 56 for the pair, profiles/r04_train_*)
+  // (AUTO keeps the pair whenever the split-bf16 GEMM runs: the fused kernels are fp32 MFMA;
+  // 2 x 100 000 pairs 57.6 ms with the pair vs 60.7 fused, profiles/r05_train_sched.txt)
   const bool fused = basic && (schedule == 1 || schedule == 3 ||
-                     (schedule == 0 && rounds >= 3 && 10 * blocks >= 9 * rounds * waves));
+                     (schedule == 0 && panel_mode() < 3 && rounds >= 3 &&
+                      10 * blocks >= 9 * rounds * waves));
   if (!fused) {
     // the residual enters the GEMM's epilogue (y = x·Wᵀ + res, its C read 4 iterations ahead),
     // so the act pass reads y and writes h instead of reading y and res and writing both back

@@ -40,13 +40,15 @@ H = 128
 # AUTO, 1 / 3 the fused kernels (one / four waves per 32-point block).  PNTF_TT_FUSED sets it
 # (to compare; profiles/r04_train_sched*.txt).
 _LINEAR_ACT = int(os.environ.get("PNTF_TT_FUSED", "2"))
-# Input gradient + the previous layer's act adjoint in one kernel (pntf_tt_linear_bwd): 1, or
-# pntf_tt_gemm then pntf_tt_act_bwd: 0; unset (None): the fused kernel for layers of at least
-# _BWD_FUSED_MIN_POINTS points (it balances only with several blocks per wave: 2 x 100 000
-# pairs 64.9 -> 63.3 ms, 2 x 10 000 6.86 -> 7.08 ms).  PNTF_TT_BWD sets it.
+# Input gradient + the previous layer's act adjoint in one kernel (pntf_tt_linear_bwd, fp32
+# MFMA): 1, or pntf_tt_gemm then pntf_tt_act_bwd: 0; unset (None): the fused kernel for layers
+# of at least _BWD_FUSED_MIN_POINTS points.  With the fp32-MFMA GEMMs the fused kernel won at
+# large batches (2 x 100 000 pairs 64.9 -> 63.3 ms); since the split-bf16 GEMMs (round 5) the
+# pair wins everywhere (2 x 100 000: 57.6 vs 59.6 ms, 2 x 10 000: 6.09 vs 6.65;
+# profiles/r05_train_sched.txt), so AUTO never takes it.  PNTF_TT_BWD sets it.
 _LINEAR_BWD = (int(os.environ["PNTF_TT_BWD"]) if os.environ.get("PNTF_TT_BWD", "") != ""
                else None)
-_BWD_FUSED_MIN_POINTS = 100000
+_BWD_FUSED_MIN_POINTS = None
 _BLOCK_HEADS = ("encoder.1", "encoder.2", "generator.0", "generator.1", "generator.2")
 
 
@@ -234,8 +236,11 @@ def _adjoint(tape, g, grads, part, merge_bwd, want_input=False):
         W = params[name + ".weight"]
         prev = order[idx + 1]
         res = pending.pop() if name in _BLOCK_HEADS else None
-        use_bwd = tape.fused and ((M >= _BWD_FUSED_MIN_POINTS) if _LINEAR_BWD is None
-                                  else bool(_LINEAR_BWD))
+        if _LINEAR_BWD is None:
+            use_bwd = tape.fused and _BWD_FUSED_MIN_POINTS is not None and \
+                M >= _BWD_FUSED_MIN_POINTS
+        else:
+            use_bwd = tape.fused and bool(_LINEAR_BWD)
         fused_in = use_bwd and name != "generator.0" and prev[3]
         if fused_in:
             # gx = act_bwd_prev(g·W (+ res)): in place into the residual branch's buffer

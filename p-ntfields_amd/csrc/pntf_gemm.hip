@@ -578,6 +578,14 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
 #ifndef PNTF_X6_TSTORE
 #define PNTF_X6_TSTORE 1
 #endif
+// Diagnostic variant (1): the A panel arrives row-contiguously (4 lanes per 64-byte row segment,
+// 16 rows per load) and reaches the MFMA layout through a per-wave LDS block two k blocks ahead
+// of its split.  Same-box A/B against the direct loads (0, shipped; one lane per row, 32 cache
+// lines per load): no difference (generator forward 175.1 vs 173.8 TFLOP/s,
+// profiles/r05_x6_gemm.txt), so the half-filled-line loads are not what binds.
+#ifndef PNTF_X6_LSTAGE
+#define PNTF_X6_LSTAGE 0
+#endif
 // diagnostics only (tests/diag/gemm_variants.py ablations; wrong results): bit 1 no operand
 // split, 2 no LDS fragment reads in the loop, 4 no next-panel loads, 8 no C stores, 16 every
 // panel load from the first tile (L2-resident), 32 the panel's bytes read row-contiguously
@@ -683,6 +691,10 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
   // layout writes and the row-contiguous reads are both conflict-free)
   __shared__ f32x4 lt[4][32 * 17];
 #endif
+#if PNTF_X6_LSTAGE
+  // per wave: one k block of the panel (32 rows x 64 bytes, row stride 5 float4: conflict-free)
+  __shared__ f32x4 lst[4][32 * 5];
+#endif
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // block b -> (group, workgroup index): the NG workgroups of a set of tiles on one XCD
@@ -718,21 +730,51 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
 #endif
   const int c0 = CG * grp;
   f32x4 x[QK];
+#if PNTF_X6_LSTAGE
+  // raw panel registers: x[2b + q] = rows 16q + (lane >> 2), bytes 64b + 16 (lane & 3) ..
+  // of the tile (k block b), staged through lst into the MFMA layout two blocks ahead
+  const int vr = (int)(((lane >> 2) * g.lda) * 4 + 16 * (lane & 3));
+  const int sq = __builtin_amdgcn_readfirstlane((int)(64 * g.lda));   // 16 rows, in bytes
+  auto raw = [&](Rsrc r, int b, int q) { return pg_load(r, vr, 64 * b + q * sq); };
+  auto stage = [&](int b, f32x4& y0, f32x4& y1) {
+    lst[w][(lane >> 2) * 5 + (lane & 3)] = x[2 * b];
+    lst[w][(16 + (lane >> 2)) * 5 + (lane & 3)] = x[2 * b + 1];
+    asm volatile("" ::: "memory");     // (compiler order; LDS itself is in order per wave)
+    y0 = lst[w][j * 5 + 2 * h];
+    y1 = lst[w][j * 5 + 2 * h + 1];
+  };
+  auto tile_win = [&](int64_t t) { return win(g.A, g.lda, t < ntiles ? t : tile); };
+  f32x4 y[2];
+  bf16x8 s[3];
+  {
+    const Rsrc ra = win(g.A, g.lda, tile);
+#pragma unroll
+    for (int q = 0; q < QK; ++q) x[q] = raw(ra, q >> 1, q & 1);
+    stage(0, y[0], y[1]);
+    x6_split(y[0], y[1], s);
+    stage(1, y[0], y[1]);
+    // blocks 0 and 1 of the next tile: staged at this tile's blocks KB - 2, KB - 1
+    const Rsrc rn = tile_win(tile + stride);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = raw(rn, q >> 1, q & 1);
+  }
+#else
   {
     const Rsrc ra = win(g.A, g.lda, tile);
 #pragma unroll
     for (int q = 0; q < QK; ++q) x[q] = pg_load(ra, va, 64 * (q >> 1) + 16 * (q & 1));
   }
+  // the split terms of the current k block; the next block's are computed beside this
+  // block's MFMAs (software pipeline, wrapping into the next tile's first block)
+  bf16x8 s[3];
+  x6_split(x[0], x[1], s);
+#endif
   const bf16x8* lf = lw + lane;
   bf16x8 fr[2][TG][3];
 #pragma unroll
   for (int t = 0; t < TG; ++t)
 #pragma unroll
     for (int p = 0; p < 3; ++p) fr[0][t][p] = lf[((t * KB) * 3 + p) * 64];
-  // the split terms of the current k block; the next block's are computed beside this
-  // block's MFMAs (software pipeline, wrapping into the next tile's first block)
-  bf16x8 s[3];
-  x6_split(x[0], x[1], s);
   for (;;) {
     const int64_t next = tile + stride;
     const bool more = next < ntiles;
@@ -784,7 +826,19 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
       // next block's terms (past the tile's end: the next panel's first block, loaded at
       // this tile's block 0)
       bf16x8 sn[3];
-#if !(PNTF_X6_ABL & 1)
+#if PNTF_X6_LSTAGE
+      // stage block kb + 2 (the next tile's 0 / 1 past the end), reload its raw registers
+      // with the tile one further, and split block kb + 1 (staged one block ago)
+      f32x4 yn[2];
+      {
+        constexpr int b2 = (kb + 2) % KB;
+        stage(b2, yn[0], yn[1]);
+        const Rsrc rr = kb + 2 < KB ? rn : tile_win(tile + 2 * stride);
+        x[2 * b2] = raw(rr, b2, 0);
+        x[2 * b2 + 1] = raw(rr, b2, 1);
+      }
+      x6_split(y[0], y[1], sn);
+#elif !(PNTF_X6_ABL & 1)
       x6_split(x[2 * kn], x[2 * kn + 1], sn);
 #else
       sn[0] = __builtin_bit_cast(bf16x8, x[2 * kn]);
@@ -806,7 +860,10 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
       }
       // x[2kb], x[2kb + 1] were split one block ago: reload them with the next panel's (the
       // last tile reloads its own: no branch in the MFMA stream)
-#if PNTF_X6_ABL & 32
+#if PNTF_X6_LSTAGE
+      y[0] = yn[0];
+      y[1] = yn[1];
+#elif PNTF_X6_ABL & 32
       // (the same bytes per tile read row-contiguously: 8 lanes per 128-byte line, 8 rows per
       // instruction; wrong operands)
       x[2 * kb] = pg_load(rn, vco, 4096 * (kb & 3) + 128 * (kb >> 2));

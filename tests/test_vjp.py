@@ -301,8 +301,9 @@ def test_epilogue_outputs_raise_on_backward_and_b_grad_raises():
 
 @pytest.mark.gpu
 def test_fused_bwd_multi_round_matches_two_kernel():
-    """the fused input-gradient kernel (pntf_tt_linear_bwd, default for layers of
-    >= 100 000 points) at a size where every workgroup strides over several 32-point blocks
+    """the fused input-gradient kernel (pntf_tt_linear_bwd; AUTO took it for layers
+    of >= 100 000 points until the split-bf16 GEMMs made the pair faster at every batch, round
+    5; PNTF_TT_BWD=1 still selects it) at a size where every workgroup strides over several 32-point blocks
     (8 192 pairs: 16 384 encoder points = 512 blocks per column group over <= 256
     workgroups) agrees with the GEMM + act pair on the loss gradients."""
     from pntf import train

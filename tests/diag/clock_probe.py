@@ -105,9 +105,18 @@ def main():
     Wt = torch.randn(N, K, device=dev)
     Y = torch.empty(rows, N, device=dev)
     GW = torch.empty(N, K, device=dev)
-    for tag, (ta, tb, M, Nn, Kk, A, lda, Bm, ldb, C, ldc) in (
-            ("gemm_forward_gen_panel_lds", (0, 1, rows, N, K, X, K, Wt, K, Y, N)),
-            ("gemm_wgrad_gen", (1, 0, N, K, rows, G, N, X, K, GW, K))):
+    # the split-bf16 kernels (the default modes) and the fp32-MFMA ones
+    lib.pntf_tt_set_panel_mode.argtypes = [ctypes.c_int]
+    lib.pntf_tt_set_wgrad_mode.argtypes = [ctypes.c_int]
+    for tag, mode, (ta, tb, M, Nn, Kk, A, lda, Bm, ldb, C, ldc) in (
+            ("gemm_forward_gen_x6", 3, (0, 1, rows, N, K, X, K, Wt, K, Y, N)),
+            ("gemm_wgrad_gen_x6", 2, (1, 0, N, K, rows, G, N, X, K, GW, K)),
+            ("gemm_forward_gen_panel_lds_fp32", 2, (0, 1, rows, N, K, X, K, Wt, K, Y, N)),
+            ("gemm_wgrad_gen_fp32", 1, (1, 0, N, K, rows, G, N, X, K, GW, K))):
+        if ta:
+            lib.pntf_tt_set_wgrad_mode(mode)
+        else:
+            lib.pntf_tt_set_panel_mode(mode)
         nw = lib.pntf_tt_gemm_work_floats(M, Nn, Kk)
         work = torch.empty(max(nw, 1), device=dev)
         ms = soak(lambda: lib.pntf_tt_gemm(ta, tb, M, Nn, Kk, V(A), lda, V(Bm), ldb, V(C), ldc,

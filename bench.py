@@ -570,6 +570,13 @@ def train_extras(dev, sizes=((2, 10000), (2, 100000)), reps=20, warm=5):
         out[tag + "_pairs_per_s"] = E * n / (ms * 1e-3)
         out[tag + "_TFLOPs_reference_equivalent"] = TRAIN_FLOP_PER_PAIR * E * n / (ms * 1e-3) / 1e12
         out[tag + "_TFLOPs_executed"] = TRAIN_FLOP_EXECUTED_PER_PAIR * E * n / (ms * 1e-3) / 1e12
+    # the GEMM arithmetic of the step: fp32 operands and results, each
+    # product as six bf16 MFMA products of three-term operand splits (fp32-level error against
+    # fp64: tests/test_train.py::test_x6_gemm_vs_fp64, profiles/r05_x6_accuracy.txt)
+    from pntf import _lib
+    out["train_gemm_arithmetic"] = (
+        "fp32 in/out, split-bf16 MFMA (3-term operands, 6 products, per-order accumulators)"
+        if _lib.load().pntf_tt_set_panel_mode(-1) == 3 else "fp32 MFMA")
     return out
 
 

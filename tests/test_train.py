@@ -553,6 +553,30 @@ def test_x6_gemm_vs_fp64(tb, M, N, K, beta):
 
 
 @pytest.mark.gpu
+def test_x6_gemm_wide_dynamic_range():
+    """The split-bf16 GEMM keeps fp32's relative accuracy when operand magnitudes span
+    1e-12..1e12 within a row (bf16 has fp32's exponent range, and each split term is taken
+    relative to its own element): elementwise within the fp32 accumulation bound of
+    (|A|·|B|) against fp64, with exact zeros mixed in."""
+    from pntf import train
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(99)
+    M, N, K = 4099, 256, 256
+    mag = lambda *s: torch.pow(10.0, (torch.rand(*s, generator=g) * 24 - 12))   # noqa: E731
+    sgn = lambda *s: torch.where(torch.rand(*s, generator=g) < 0.5, -1.0, 1.0)   # noqa: E731
+    A = (mag(M, K) * sgn(M, K)).float()
+    A[torch.rand(M, K, generator=g) < 0.05] = 0.0
+    B = (mag(N, K) * sgn(N, K)).float()
+    C = torch.empty(M, N, device=dev)
+    train.gemm(C, A.to(dev), B.to(dev), False, True, 0.0)
+    ref = A.double() @ B.double().t()
+    scale = A.double().abs() @ B.double().abs().t()
+    err = (C.cpu().double() - ref).abs()
+    assert torch.isfinite(C).all()
+    assert torch.all(err <= 1e-5 * np.sqrt(K) * scale + 1e-30), float((err / scale).max())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fused", [1, 3])
 @pytest.mark.parametrize("dim", [3, 6])
 @pytest.mark.parametrize("n", [1, 77, 333])

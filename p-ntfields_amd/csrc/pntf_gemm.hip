@@ -586,6 +586,11 @@ __global__ __launch_bounds__(256, 1) void panel_lds_kernel(PanelArgs g) {
 #ifndef PNTF_X6_LSTAGE
 #define PNTF_X6_LSTAGE 0
 #endif
+// 1: reload a panel block's registers in the block that splits them (one k block more lead
+// for the next tile's loads); 0: one block later
+#ifndef PNTF_X6_EARLY
+#define PNTF_X6_EARLY 0
+#endif
 // diagnostics only (tests/diag/gemm_variants.py ablations; wrong results): bit 1 no operand
 // split, 2 no LDS fragment reads in the loop, 4 no next-panel loads, 8 no C stores, 16 every
 // panel load from the first tile (L2-resident), 32 the panel's bytes read row-contiguously
@@ -691,6 +696,9 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
   // layout writes and the row-contiguous reads are both conflict-free)
   __shared__ f32x4 lt[4][32 * 17];
 #endif
+#if PNTF_X6_LSTAGE && PNTF_X6_EARLY
+#error "PNTF_X6_EARLY applies to the direct panel loads"
+#endif
 #if PNTF_X6_LSTAGE
   // per wave: one k block of the panel (32 rows x 64 bytes, row stride 5 float4: conflict-free)
   __shared__ f32x4 lst[4][32 * 5];
@@ -768,6 +776,14 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
   // block's MFMAs (software pipeline, wrapping into the next tile's first block)
   bf16x8 s[3];
   x6_split(x[0], x[1], s);
+#if PNTF_X6_EARLY
+  {   // block 0 of the next tile (split at this tile's last block)
+    const int64_t t1 = tile + stride;
+    const Rsrc r1 = win(g.A, g.lda, t1 < ntiles ? t1 : tile);
+    x[0] = pg_load(r1, va, 0);
+    x[1] = pg_load(r1, va, 16);
+  }
+#endif
 #endif
   const bf16x8* lf = lw + lane;
   bf16x8 fr[2][TG][3];
@@ -840,6 +856,14 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
       x6_split(y[0], y[1], sn);
 #elif !(PNTF_X6_ABL & 1)
       x6_split(x[2 * kn], x[2 * kn + 1], sn);
+#if PNTF_X6_EARLY
+      {   // x[2kn], x[2kn + 1] are dead now: the next tile's block kn (the one after for kn = 0)
+        const int64_t t2 = tile + 2 * stride;
+        const Rsrc rr = kn != 0 ? rn : win(g.A, g.lda, t2 < ntiles ? t2 : tile);
+        x[2 * kn] = pg_load(rr, va, 64 * kn);
+        x[2 * kn + 1] = pg_load(rr, va, 64 * kn + 16);
+      }
+#endif
 #else
       sn[0] = __builtin_bit_cast(bf16x8, x[2 * kn]);
       sn[1] = __builtin_bit_cast(bf16x8, x[2 * kn + 1]);
@@ -868,7 +892,7 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
       // instruction; wrong operands)
       x[2 * kb] = pg_load(rn, vco, 4096 * (kb & 3) + 128 * (kb >> 2));
       x[2 * kb + 1] = pg_load(rn, vco, 4096 * (kb & 3) + 128 * (kb >> 2) + 64);
-#elif !(PNTF_X6_ABL & 4)
+#elif !(PNTF_X6_ABL & 4) && !PNTF_X6_EARLY
       x[2 * kb] = pg_load(rn, va, 64 * kb);
       x[2 * kb + 1] = pg_load(rn, va, 64 * kb + 16);
 #endif

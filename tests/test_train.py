@@ -192,6 +192,7 @@ def test_two_adamw_steps_vs_reference(name, dim):
     values or against the exact (fp64) trajectory, with the same bound."""
     from pntf.train import AdamW
     dev = torch.device("cuda:0")
+    case = name
     W = _case_weights(name)
     f = load(name)
     g64, loss2_64, after64 = _f64_two_steps(name)
@@ -236,10 +237,15 @@ def test_two_adamw_steps_vs_reference(name, dim):
                 err = np.abs(got - target)
                 delta = 2 * max(float(np.abs(grads[0][name] - gref).max()), 1e-12)
                 bound = 2e-6 + 8 * lr * delta / np.maximum(g, delta)
-                ok |= err <= bound
                 if worst is None:
                     i = np.argmax(err - bound)
                     worst = (float(err.flat[i]), float(bound.flat[i]))
+                    vs_ref = err <= bound
+                ok |= err <= bound
+            if not vs_ref.all():   # printed: which elements needed the exact trajectory
+                print("two-step %s %s: %d element(s) outside the bound of the reference's fp32 "
+                      "values, within that of the fp64 trajectory" % (case, name,
+                                                                       int((~vs_ref).sum())))
             assert ok.all(), (name, int((~ok).sum()), worst)
     assert np.array_equal(sd["encoder1.0.weight"].detach().cpu().numpy(), W["encoder1.0.weight"])
 

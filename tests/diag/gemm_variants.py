@@ -28,7 +28,12 @@ def main(names, pairs=20000, check=True):
     shapes = (("gen", 13 * pairs, 256, 256), ("enc", 14 * pairs, 128, 128),
               ("enc0", 14 * pairs, 256, 128))
     for name in names:
-        lib = ctypes.CDLL(os.path.join(HERE, "libgemm_%s.so" % name))
+        # "<lib>@<mode>": libgemm_<lib>.so with pntf_tt_set_panel_mode(<mode>)
+        lname, _, mode = name.partition("@")
+        lib = ctypes.CDLL(os.path.join(HERE, "libgemm_%s.so" % lname))
+        if mode:
+            lib.pntf_tt_set_panel_mode.argtypes = [ctypes.c_int]
+            lib.pntf_tt_set_panel_mode(int(mode))
         lib.pntf_tt_gemm_work_floats.restype = ctypes.c_size_t
         lib.pntf_tt_gemm_work_floats.argtypes = [ctypes.c_int64] * 3
         lib.pntf_tt_gemm.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_int64] * 3 + \

@@ -313,14 +313,15 @@ int pntf_tt_head_loss(int dim, int arm, const float* v, const float* w4, const f
  * environment, read once, or pntf_tt_set_panel_mode): 0 = none, 1 = fp32 MFMA with the
  * weight streamed from L2, 2 = fp32 MFMA with the weight in LDS, 3 (default) = the split-bf16
  * kernel (every fp32 operand as three bf16 terms, six bf16 MFMA products per fp32 product:
- * fp32 accuracy at 2.67x the fp32 MFMA rate; 1.5*K*N work floats). */
+ * fp32 accuracy at 2.67x the fp32 MFMA rate; 1.5*K*N work floats), 8 = its 16x16x32 variant
+ * with two waves per SIMD (diagnostic; 4..7 are diagnostic forms of 3 as well). */
 size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K);
 int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                  const float* B, int64_t ldb, float* C, int64_t ldc, float beta, float* work,
                  size_t work_floats, hipStream_t stream);
 const char* pntf_tt_gemm_last_error(void);
 /* Process-wide panel-kernel choice (see pntf_tt_gemm; not thread-safe against concurrent
- * GEMMs); returns the previous mode, leaves it unchanged for a mode outside 0..3. */
+ * GEMMs); returns the previous mode, leaves it unchanged for a mode outside 0..8. */
 int pntf_tt_set_panel_mode(int mode);
 /* The same for the weight-gradient shapes (ta, not tb, beta 0, M and N in {128, 256};
  * PNTF_GEMM_WGRAD in the environment): 0 = the LDS-tiled kernel, 1 = the fp32-MFMA wgrad

@@ -953,6 +953,160 @@ __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g)
 }
 
 // ---------------------------------------------------------------------------------------
+// Split-bf16 panel GEMM on 16 x 16 x 32 tiles, two waves per SIMD (`panel_x6s_kernel`).
+// panel_x6_kernel runs one wave per SIMD: its 32-row panel (128 VGPRs at K = 256) and the
+// per-order accumulators leave no room for a second wave, so each next-panel load's latency is
+// hidden only by the wave's own MFMAs.  Here a wave owns 16 rows (the B operand of
+// v_mfma_f32_16x16x32_bf16: lane l holds panel row l & 15, k = 8(l >> 4) .. +7 of the 32-k
+// block), so the panel takes 64 VGPRs and eight waves (two per SIMD) share the workgroup's
+// weight group in LDS.  A operand: lane l holds W(out col 16t + (l & 15), k = 8(l >> 4) + j),
+// three bf16 terms per 1 KiB fragment (x6s_pack_kernel).  D register i of lane l is out col
+// c0 + 16t + 4(l >> 4) + i of row l & 15.  Each panel load covers 16 rows x 128 contiguous
+// bytes (one cache line per row).  Same splits, products and per-order accumulation
+// (V = 1: a0b0 | the five smaller products) as panel_x6_kernel.  Selected by panel mode 8
+// (PNTF_GEMM_PANEL=8 / pntf_tt_set_panel_mode).  Same-box A/B (tests/diag/gemm_variants.py,
+// profiles/r05_x6_gemm.txt): the generator GEMMs within noise of panel_x6_kernel (172-175 vs
+// 165-172 TFLOP/s), some encoder shapes slower, so mode 3 stays the default: latency hiding is
+// not what binds these kernels (the split-bf16 GEMMs also run at 1.77-1.88 GHz against the
+// fp32-MFMA kernels' 2.3, profiles/r05_clock_probe.txt).
+constexpr int X6S_CG = 64;   // columns per workgroup (4 out tiles of 16)
+
+// P[((t·KB + kb)·3 + p)·64 + lane] = term p of B(32 kb + 8 (lane >> 4) + j, 16 t + (lane & 15))
+__global__ void x6s_pack_kernel(const float* __restrict__ W, int64_t ldb, int tb, int KC, int NC,
+                                bf16x8* __restrict__ P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int KB = KC / 32;
+  if (i >= (int64_t)(NC / 16) * KB * 64) return;
+  const int lane = (int)(i & 63), kb = (int)((i >> 6) % KB), nt = (int)((i >> 6) / KB);
+  const int n = 16 * nt + (lane & 15), k0 = 32 * kb + 8 * (lane >> 4);
+  f32x4 a, b;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = tb ? W[(int64_t)n * ldb + k0 + e] : W[(int64_t)(k0 + e) * ldb + n];
+    b[e] = tb ? W[(int64_t)n * ldb + k0 + 4 + e] : W[(int64_t)(k0 + 4 + e) * ldb + n];
+  }
+  bf16x8 sp[3];
+  x6_split(a, b, sp);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) P[((int64_t)(nt * KB + kb) * 3 + p) * 64 + lane] = sp[p];
+}
+
+__device__ __forceinline__ f32x4 mfma16bf(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int KC, int NC, bool ACC>
+__global__ __launch_bounds__(512, 1) void panel_x6s_kernel(PanelArgs g) {
+  PNTF_CLOCK_SCOPE;
+  constexpr int KB = KC / 32, QK = KC / 8, CG = X6S_CG, TG = CG / 16, NG = NC / CG;
+  constexpr int FR = TG * KB * 3;   // 1 KiB fragments per group
+  constexpr int NW = 8;             // waves per workgroup
+  static_assert(KB >= 4, "C prefetch distance");
+  __shared__ bf16x8 lw[FR * 64];
+  __shared__ f32x4 lb[ACC ? CG / 4 : 1];
+  const int lane = threadIdx.x & 63, r = lane & 15, q4 = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int grp = 0, wg = blockIdx.x, nwg = gridDim.x;
+  if constexpr (NG > 1) {   // the NG workgroups of a set of tiles on one XCD
+    const int x = blockIdx.x & 7, sb = blockIdx.x >> 3;
+    grp = sb % NG;
+    wg = (sb / NG) * 8 + x;
+    nwg = gridDim.x / NG;
+  }
+  {
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(g.P) + (int64_t)grp * FR * 64;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < FR * 64; i += 64 * NW) lw[i] = src[i];
+    if (ACC && g.bias && threadIdx.x < CG / 4)
+      lb[threadIdx.x] = *reinterpret_cast<const f32x4*>(g.bias + CG * grp + 4 * threadIdx.x);
+  }
+  __syncthreads();
+  const int64_t ntiles = (g.M + 15) / 16;
+  const int64_t stride = (int64_t)nwg * NW;
+  int64_t tile = (int64_t)wg * NW + w;
+  if (tile >= ntiles) return;   // wave-uniform; no barrier follows
+  auto win = [&](const float* base, int64_t ld, int64_t t) {
+    const int64_t rows = g.M - 16 * t;
+    return pg_rsrc(base + 16 * t * ld, (rows < 16 ? rows : 16) * ld * 4);
+  };
+  const int va = (int)((r * g.lda + 8 * q4) * 4), vc = (int)((r * g.ldc + 4 * q4) * 4);
+  const int c0 = CG * grp;
+  // panel: x[2kb], x[2kb + 1] = row r, k = 32 kb + 8 q4 .. +7
+  f32x4 x[KB * 2];
+  {
+    const Rsrc ra = win(g.A, g.lda, tile);
+#pragma unroll
+    for (int q = 0; q < 2 * KB; ++q) x[q] = pg_load(ra, va, 128 * (q >> 1) + 16 * (q & 1));
+  }
+  const bf16x8* lf = lw + lane;
+  bf16x8 fr[2][TG][3];
+#pragma unroll
+  for (int t = 0; t < TG; ++t)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) fr[0][t][p] = lf[((t * KB) * 3 + p) * 64];
+  bf16x8 s[3];
+  x6_split(x[0], x[1], s);
+  for (;;) {
+    const int64_t next = tile + stride;
+    const bool more = next < ntiles;
+    const Rsrc rn = win(g.A, g.lda, more ? next : tile);
+    const Rsrc rc = win(g.C, g.ldc, tile), rci = win(g.Cin, g.ldc, tile);
+    f32x4 acc[TG], accl[TG], cb[TG];
+#pragma unroll
+    for (int t = 0; t < TG; ++t) {
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      accl[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    pg_static_for<0, KB>([&](auto I) {
+      constexpr int kb = decltype(I)::value, cur = kb & 1;
+      if constexpr (ACC && kb == KB - 4) {
+#pragma unroll
+        for (int t = 0; t < TG; ++t) cb[t] = pg_load(rci, vc, (c0 + 16 * t) * 4);
+      }
+      constexpr int kn = (kb + 1) % KB;
+#pragma unroll
+      for (int t = 0; t < TG; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fr[cur ^ 1][t][p] = lf[((t * KB + kn) * 3 + p) * 64];
+      bf16x8 sn[3];
+      x6_split(x[2 * kn], x[2 * kn + 1], sn);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) {
+        const bf16x8 (&a)[3] = fr[cur][t];
+        f32x4 l = accl[t];
+        l = mfma16bf(a[2], s[0], l);
+        l = mfma16bf(a[1], s[1], l);
+        l = mfma16bf(a[0], s[2], l);
+        l = mfma16bf(a[1], s[0], l);
+        l = mfma16bf(a[0], s[1], l);
+        accl[t] = l;
+        acc[t] = mfma16bf(a[0], s[0], acc[t]);
+      }
+      // x[2kb], x[2kb + 1] were split one block ago: the next panel's
+      x[2 * kb] = pg_load(rn, va, 128 * kb);
+      x[2 * kb + 1] = pg_load(rn, va, 128 * kb + 16);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) s[p] = sn[p];
+      if constexpr (kb == KB - 1) {
+        const bool brow = ACC && g.bias && 16 * tile + r < g.brows;
+#pragma unroll
+        for (int t = 0; t < TG; ++t) {
+          f32x4 v = acc[t] + accl[t];
+          if (ACC) {
+            if (brow) v += lb[4 * t + q4];
+            v += cb[t];
+          }
+          pg_store(rc, v, vc, (c0 + 16 * t) * 4);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (!more) break;
+    tile = next;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Linear + act_laplace of the Taylor tape in one pass (pntf_tt_linear_act; the forward of one
 // Linear of NN.out_laplace, model_res_sigmoid_multi.py:710-848 with act_laplace :675-691).
 // The LDS panel GEMM above with the tape's elementwise stage as its epilogue, so the
@@ -1746,7 +1900,7 @@ int g_panel_mode = -1;
 int panel_mode() {
   if (g_panel_mode < 0) {
     const char* e = getenv("PNTF_GEMM_PANEL");
-    g_panel_mode = e && e[0] >= '0' && e[0] <= '7' ? e[0] - '0' : 3;
+    g_panel_mode = e && e[0] >= '0' && e[0] <= '8' ? e[0] - '0' : 3;
   }
   return g_panel_mode;
 }
@@ -1828,7 +1982,7 @@ int pntf_tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A
 
 int pntf_tt_set_panel_mode(int mode) {
   const int prev = panel_mode();
-  if (mode >= 0 && mode <= 7) g_panel_mode = mode;
+  if (mode >= 0 && mode <= 8) g_panel_mode = mode;
   return prev;
 }
 
@@ -1857,9 +2011,36 @@ static int tt_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, const float*
     return PNTF_ERR_ARG;
   }
   const int pm = panel_mode();
+  if (panel_path(ta, N, K, lda, ldc, beta, A, C, work, work_floats) && pm == 8) {
+    // the 16 x 16 x 32 split-bf16 panel kernel, eight waves per workgroup
+    const int64_t nf = (N / 16) * (K / 32) * 64;
+    hipLaunchKernelGGL(x6s_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream,
+                       B, ldb, tb, (int)K, (int)N, reinterpret_cast<bf16x8*>(work));
+    PanelArgs p{A, reinterpret_cast<const f32x4*>(work), C, M, lda, ldc, Cin, bias, brows};
+    const int64_t tiles = (M + 15) / 16, wgs = (tiles + 7) / 8;
+    const int64_t ng = N / X6S_CG, cap = num_cus() / ng;
+    int64_t nwg = wgs < cap ? wgs : cap;
+    if (ng > 1) nwg = (nwg + 7) / 8 * 8;
+    const dim3 grid((unsigned)(nwg * ng));
+#define PNTF_PANEL(KC, NC)                                                                      \
+  if (beta != 0.f) hipLaunchKernelGGL((panel_x6s_kernel<KC, NC, true>), grid, dim3(512), 0,      \
+                                      stream, p);                                               \
+  else hipLaunchKernelGGL((panel_x6s_kernel<KC, NC, false>), grid, dim3(512), 0, stream, p);
+    if (K == 128 && N == 128) { PNTF_PANEL(128, 128) }
+    else if (K == 128) { PNTF_PANEL(128, 256) }
+    else if (N == 128) { PNTF_PANEL(256, 128) }
+    else { PNTF_PANEL(256, 256) }
+#undef PNTF_PANEL
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "pntf_tt_gemm: %s", hipGetErrorString(e));
+      return PNTF_ERR_HIP;
+    }
+    return PNTF_OK;
+  }
   // modes 4 / 5 (diagnostics): the split kernel for the forward (tb) / input-gradient (!tb)
   // GEMMs only; 6 / 7: its accumulation variants V = 0 / 1
-  const bool x6 = pm == 3 || pm >= 6 || (pm == 4 && tb) || (pm == 5 && !tb);
+  const bool x6 = pm == 3 || pm == 6 || pm == 7 || (pm == 4 && tb) || (pm == 5 && !tb);
   if (panel_path(ta, N, K, lda, ldc, beta, A, C, work, work_floats) && x6) {
     const int64_t nf = (N / 32) * (K / 16) * 64;
     hipLaunchKernelGGL(x6_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream,

@@ -523,8 +523,9 @@ def test_mfma_gemm_vs_fp64(ta, tb, M, N, K, beta):
     (False, 1, 256, 128, 0.0),
 ])
 def test_x6_gemm_vs_fp64(tb, M, N, K, beta):
-    """The split-bf16 panel kernel (panel_x6_kernel: every fp32 operand as three bf16 terms,
-    six bf16 MFMA products per fp32 product) against an fp64 matmul of the same fp32 operands,
+    """The split-bf16 panel kernels (panel_x6_kernel: every fp32 operand as three bf16 terms,
+    six bf16 MFMA products per fp32 product; panel_x6s_kernel, its 16 x 16 x 32 variant with
+    two waves per SIMD, PNTF_GEMM_PANEL=8) against an fp64 matmul of the same fp32 operands,
     beside the fp32-MFMA LDS panel kernel on the same call: elementwise within the fp32
     accumulation bound 1e-5·sqrt(K)·(|A|·|B|), and its error statistics no worse than fp32's
     (mean relative error within 1.5x, max within 2x)."""
@@ -542,7 +543,8 @@ def test_x6_gemm_vs_fp64(tb, M, N, K, beta):
     rel = {}
     prev = lib.pntf_tt_set_panel_mode(3)
     try:
-        for mode in (2, 3):
+        # 2: fp32 MFMA; 3: split bf16 (default); 8: its 16 x 16 x 32, two-waves-per-SIMD variant
+        for mode in (2, 3, 8):
             lib.pntf_tt_set_panel_mode(mode)
             C = C0.to(dev)
             train.gemm(C, Ad, Bd, False, tb, beta)
@@ -551,11 +553,12 @@ def test_x6_gemm_vs_fp64(tb, M, N, K, beta):
             rel[mode] = err / scale
     finally:
         lib.pntf_tt_set_panel_mode(prev)
-    m2, m3 = float(rel[2].mean()), float(rel[3].mean())
-    x2, x3 = float(rel[2].max()), float(rel[3].max())
-    print("x6 gemm %s M=%d N=%d K=%d: mean rel err fp32 %.3g x6 %.3g, max %.3g / %.3g"
-          % ("fwd" if tb else "bwd", M, N, K, m2, m3, x2, x3))
+    m2, m3, m8 = (float(rel[m].mean()) for m in (2, 3, 8))
+    x2, x3, x8 = (float(rel[m].max()) for m in (2, 3, 8))
+    print("x6 gemm %s M=%d N=%d K=%d: mean rel err fp32 %.3g x6 %.3g x6s %.3g, max %.3g / %.3g "
+          "/ %.3g" % ("fwd" if tb else "bwd", M, N, K, m2, m3, m8, x2, x3, x8))
     assert m3 <= 1.5 * m2 + 1e-12 and x3 <= 2.0 * x2 + 1e-12
+    assert m8 <= 1.5 * m2 + 1e-12 and x8 <= 2.0 * x2 + 1e-12
 
 
 @pytest.mark.gpu

@@ -36,6 +36,7 @@ __global__ void copy_kernel(const float* __restrict__ src, int n, float* __restr
 __global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int cols, int ld,
                                  int trans, float scale, float* __restrict__ dst);
 __global__ void pack_wide_aux_kernel(const float* __restrict__ plain, float* __restrict__ wide);
+__global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restrict__ x6);
 __global__ void pack_quad_kernel(const float* __restrict__ src, int rows, int cols, int dir,
                                  float* __restrict__ dst);
 __global__ void pack_quad_aux_kernel(const float* __restrict__ plain, float* __restrict__ quad);
@@ -286,7 +287,7 @@ const char* pntf_status_string(int status) {
 
 const char* pntf_last_error(void) { return g_err; }
 
-size_t pntf_packed_floats(void) { return (size_t)PACKED_TOTAL; }
+size_t pntf_packed_floats(void) { return (size_t)PACKED_TOTAL_X6; }
 
 const char* pntf_build_info(void) { return PNTF_BUILD_INFO; }
 
@@ -333,7 +334,7 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
       {28, 256, 256, OFF_GBLK + 5 * SZ_G},                    // generator1.2
       {20, 128, 256, OFF_G3},                                 // generator.3
   };
-  hipMemsetAsync(packed, 0, sizeof(float) * PACKED_TOTAL, stream);
+  hipMemsetAsync(packed, 0, sizeof(float) * PACKED_TOTAL_X6, stream);
   for (int m = 0; m < (int)(sizeof(mats) / sizeof(mats[0])); ++m) {
     const M& d = mats[m];
     int64_t cnt = (int64_t)d.rows * d.cols;
@@ -373,6 +374,10 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
                      packed + OFF_BIAS, packed + OFF_WIDE);
   hipLaunchKernelGGL(pack_quad_aux_kernel, dim3(Q_WAVES * Q_NAUX), dim3(256), 0, stream,
                      packed + OFF_BIAS, packed + OFF_QUAD);
+  // the wide kernels' split-bf16 layers read a regrouped, pre-split copy of both directions
+  const int64_t nx6 = (int64_t)(2 * SZ_DIR / 1024) * 2 * 64;
+  hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)((nx6 + 255) / 256)), dim3(256), 0, stream,
+                     packed + OFF_WIDE, reinterpret_cast<uint16_t*>(packed + OFF_X6));
   return check_launch("pack_weights");
 }
 
@@ -383,7 +388,7 @@ struct pntf_net {
 
 pntf_net* pntf_net_create(const float* const* params, int n_params, hipStream_t stream) {
   float* p = nullptr;
-  if (hipMalloc(&p, sizeof(float) * PACKED_TOTAL) != hipSuccess) {
+  if (hipMalloc(&p, sizeof(float) * PACKED_TOTAL_X6) != hipSuccess) {
     fail(PNTF_ERR_HIP, "pntf_net_create: hipMalloc of the packed weights failed%s");
     return nullptr;
   }

@@ -100,6 +100,12 @@ constexpr int OFF_QUAD = (OFF_WIDE + W_SZ + 63) / 64 * 64;
 constexpr int Q_OFF_AUX = Q_WAVES * Q_STREAM;
 constexpr int Q_SZ = Q_OFF_AUX + Q_WAVES * Q_NAUX * 256;
 constexpr int PACKED_TOTAL = OFF_QUAD + Q_SZ;
+// Split-bf16 wide fragments (pntf_wide.h, PNTF_WIDE_X6): the wide region's two directions
+// regrouped per 32 x 32 step into 2 k blocks x 3 bf16 terms (1.5x the fp32 bytes; a matrix at
+// fp32 wide offset o sits at 1.5 o here)
+constexpr int OFF_X6 = (PACKED_TOTAL + 63) / 64 * 64;
+constexpr int X6_SZ = 3 * SZ_DIR;
+constexpr int PACKED_TOTAL_X6 = OFF_X6 + X6_SZ;
 // Quad layer list in stream order: packed matrix (0..12, the OFF_* order above), direction
 // (0: A = W, 1: A = W^T), out rows, in features, plain bias offset (forward layers).
 struct QLayer {

@@ -151,7 +151,10 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 constexpr int PF_STEPS = PNTF_PF_STEPS;
-constexpr int RING_NL = 4;   // fragments per step, at most
+#ifndef PNTF_RING_NL
+#define PNTF_RING_NL 4
+#endif
+constexpr int RING_NL = PNTF_RING_NL;   // fragments per step, at most (6: pntf_wide.h x6 layers)
 // Pipelined call sites (bits of PNTF_STEP_FENCE).
 constexpr int SITE_FWD_E0 = 1, SITE_FWD_ENC = 2, SITE_FWD_GEN = 4, SITE_BWD_GEN = 8,
               SITE_BWD_ENC = 16, SITE_FOLD = 32, SITE_TAYLOR = 64;

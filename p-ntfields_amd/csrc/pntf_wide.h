@@ -38,6 +38,65 @@ __device__ __forceinline__ f32x16 zero16() {
   for (int r = 0; r < 16; ++r) z[r] = 0.f;
   return z;
 }
+
+// ---------------------------------------------------------------- split-bf16 layers (x6)
+// PNTF_WIDE_X6 = 1: the generic layers (wlayer: the encoder and generator blocks, encoder[-1],
+// generator[-2] and their transposes, 90 % of the MFMA work) run each fp32 product as six
+// v_mfma_f32_32x32x16_bf16 on three-term bf16 splits of both operands (the training GEMMs'
+// scheme, pntf_gemm.hip x6_split: 2.67x the fp32 MFMA rate).  A 32-feature tile's registers
+// 8b..8b+7 are the B operand of k block b as they are (lane (j, h) holds feature rows
+// wrow(8b + i, h), i = 0..7); the weights are pre-split in the same k order (OFF_X6,
+// pack_x6_kernel).  encoder[0] and the Fourier fold stay on fp32 MFMA.
+#ifndef PNTF_WIDE_X6
+#define PNTF_WIDE_X6 0
+#endif
+constexpr int WNL = PNTF_WIDE_X6 ? 6 : 4;   // weight fragments per wlayer step
+static_assert(WNL <= RING_NL, "x6 layers read 6 fragments per step: build with PNTF_RING_NL=6");
+typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 wbf16x2 __attribute__((ext_vector_type(2)));
+typedef float wf32x2 __attribute__((ext_vector_type(2)));
+// three-term RNE split of registers 8b..8b+7 of a tile (x = x0 + x1 + x2, each bf16)
+template <bool OPAQUE = false>
+__device__ __forceinline__ void wx6_split(const f32x16& v, int b, wbf16x8 (&s)[3]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    wf32x2 x = {v[8 * b + 2 * i], v[8 * b + 2 * i + 1]};
+    // per step: the split is not shared between the out tiles of a layer (that would keep a
+    // whole split input bank live, 192 registers)
+    if constexpr (OPAQUE) asm volatile("" : "+v"(x));
+    const wbf16x2 p0 = __builtin_convertvector(x, wbf16x2);
+    const wf32x2 r1 = x - __builtin_convertvector(p0, wf32x2);
+    const wbf16x2 p1 = __builtin_convertvector(r1, wbf16x2);
+    const wf32x2 r2 = r1 - __builtin_convertvector(p1, wf32x2);
+    const wbf16x2 p2 = __builtin_convertvector(r2, wbf16x2);
+    s[0][2 * i] = p0[0]; s[0][2 * i + 1] = p0[1];
+    s[1][2 * i] = p1[0]; s[1][2 * i + 1] = p1[1];
+    s[2][2 * i] = p2[0]; s[2][2 * i + 1] = p2[1];
+  }
+}
+// out tiles per group of an x6 layer: G accumulators of NC tiles live
+#ifndef PNTF_X6_G1
+#define PNTF_X6_G1 4
+#endif
+#ifndef PNTF_X6_G2
+#define PNTF_X6_G2 1
+#endif
+#ifndef PNTF_X6_G1BUF
+#define PNTF_X6_G1BUF 1
+#endif
+constexpr int wx6_group(int OT, int NC) { return NC == 2 ? PNTF_X6_G2 : (OT < PNTF_X6_G1 ? OT : PNTF_X6_G1); }
+// the six products of order >= 2^-16, the small ones first
+__device__ __forceinline__ f32x16 wx6_mma(const f32x4& w0, const f32x4& w1, const f32x4& w2,
+                                          const wbf16x8 (&x)[3], f32x16 acc) {
+  const wbf16x8 a0 = __builtin_bit_cast(wbf16x8, w0), a1 = __builtin_bit_cast(wbf16x8, w1),
+                a2 = __builtin_bit_cast(wbf16x8, w2);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, x[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, x[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, x[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, x[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, x[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, x[0], acc, 0, 0, 0);
+}
 // Activations carried pre-scaled by κ = 10/ln 2 (round 4).  The forward pass keeps
 // y' = κ·y and h' = κ·h: encoder[0]'s weights and every forward bias column are packed times κ
 // (pack_wide_kernel / pack_wide_aux_kernel), the interior layers' weights are not (W·h' + κ·b
@@ -163,11 +222,21 @@ constexpr int WBC = (OFF_WIDE + W_OFF_BCOL) * 4;
 constexpr int WHW = (OFF_WIDE + W_OFF_G4W) * 4;
 constexpr int WG4B = (OFF_WIDE + W_OFF_G4B) * 4;
 
-// standard layer: step st = ot·KT + kt reads fragments (ot, kt, u = l)
+// standard layer: step st = ot·KT + kt reads fragments (ot, kt, u = l); base is the layer's
+// byte offset in the fp32 wide region.  x6: fragments (ot, kt, 3b + term) of the split copy
 struct WHead {
   int base;
-  __device__ int operator()(int j, int l) const { return base + (j * 4 + l) * 1024; }
+  __device__ int operator()(int j, int l) const {
+#if PNTF_WIDE_X6
+    return OFF_X6 * 4 + (base - OFF_WIDE * 4) / 2 * 3 + (j * 6 + l) * 1024;
+#else
+    return base + (j * 4 + l) * 1024;
+#endif
+  }
 };
+// fragments per step of whatever a step sequence hands over to (a WHead is always a wlayer)
+template <class F>
+constexpr int wnext_nl() { return std::is_same<F, WHead>::value ? WNL : 4; }
 // encoder[0] on Fourier features, k-tile outer: step st = kt·4 + ot (KT = 8)
 struct WE0Head {
   __device__ int operator()(int j, int l) const {
@@ -186,6 +255,7 @@ struct WFoldHead {
 };
 
 // ---------------------------------------------------------------- generic wide layer
+#if !PNTF_WIDE_X6
 // One Linear layer over OT out tiles x KT input tiles, NC columns (points) sharing the
 // weights; bank index of column c, tile t is c·OT + t (out) / c·KT + t (in).  Step st =
 // (ot, kt) runs 16·NC MFMAs on the 4 fragments of (ot, kt).  ly.init(ot, acc) starts out
@@ -195,10 +265,11 @@ template <int OT, int KT, int NC, int SITE, int NLN, class L, class PreF, class 
 __device__ __forceinline__ void wlayer(Ring& ring, Rsrc W, int wbase, const f32x16 (&in)[8],
                                        int lane, L& ly, PreF pre, NextF naddr) {
   static_assert(NC * KT <= 8 && NC * OT <= 8, "bank size");
+  static_assert(NLN == 4, "the next step sequence's width comes from its head type");
   constexpr int STEPS = OT * KT;
   constexpr bool DEF = L::DEFER;          // epilogue deferred past the next tile's first step
   f32x16 acc[DEF ? 2 : 1][NC];
-  run_steps<STEPS, 4, NLN, SITE>(
+  run_steps<STEPS, 4, wnext_nl<NextF>(), SITE>(
       ring, W, lane * 16, WHead{wbase}, naddr, [&](auto st, const f32x4 (&a)[4]) {
         constexpr int S = decltype(st)::value;
         constexpr int ot = S / KT, kt = S % KT, p = DEF ? (ot & 1) : 0;
@@ -220,6 +291,54 @@ __device__ __forceinline__ void wlayer(Ring& ring, Rsrc W, int wbase, const f32x
         }
       });
 }
+
+#else
+// x6 layer: out tiles in groups of G (wx6_group); step (g, kt, o) runs the six split products
+// of k blocks 0 and 1 of input tile kt for out tile g·G + o, so input tile kt is split once
+// per group (at o = 0) instead of once per out tile, and G accumulators are live.  The
+// fragments are packed in this step order (pack_x6_kernel).  ly.init(ot) starts tile ot at
+// its group's kt = 0 (bias MFMA, residual; a reverse layer's σ tile load into out[ot]);
+// ly.epi(ot) runs one step after the tile's last MFMAs (the last tile's at once).
+template <int OT, int KT, int NC, int SITE, int NLN, class L, class PreF, class NextF>
+__device__ __forceinline__ void wlayer(Ring& ring, Rsrc W, int wbase, const f32x16 (&in)[8],
+                                       int lane, L& ly, PreF pre, NextF naddr) {
+  static_assert(NC * KT <= 8 && NC * OT <= 8, "bank size");
+  static_assert(NLN == 4, "the next step sequence's width comes from its head type");
+  constexpr int G = wx6_group(OT, NC), STEPS = OT * KT;
+  static_assert(OT % G == 0, "out tile groups");
+  // accumulator buffers: one per tile of the group (G = 1 with PNTF_X6_G1BUF = 2: two,
+  // alternating per tile, so the deferred epilogue of the previous tile reads the other one;
+  // with 1 the previous tile's epilogue runs before the next tile starts)
+  constexpr int NB = G == 1 ? PNTF_X6_G1BUF : G;
+  f32x16 acc[NB][NC];
+  wbf16x8 xs[NC][2][3];
+  run_steps<STEPS, 6, wnext_nl<NextF>(), SITE>(
+      ring, W, lane * 16, WHead{wbase}, naddr, [&](auto st, const f32x4 (&a)[6]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int g = S / (KT * G), kt = (S / G) % KT, oo = S % G, ot = g * G + oo;
+        // accumulator buffer of this tile and of the previous group's last tile
+        constexpr int o = G == 1 ? (g % NB) : oo, last = G == 1 ? ((g + 1) % NB) : G - 1;
+        if constexpr (NB == 1 && kt == 0 && g > 0) ly.epi(ot - 1, acc[0]);
+        if constexpr (S == 0) ly.start();
+        pre(st);
+        if constexpr (oo == 0) {   // the group's first tile: split input tile kt
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) wx6_split<true>(in[c * KT + kt], b, xs[c][b]);
+        }
+        if constexpr (kt == 0) ly.init(ot, acc[o]);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+            acc[o][c] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs[c][b], acc[o][c]);
+        if constexpr (G > 1 && kt == KT - 1 && oo > 0) ly.epi(ot - 1, acc[o - 1]);
+        if constexpr (NB > 1 && kt == 0 && oo == 0 && g > 0) ly.epi(ot - 1, acc[last]);
+        if constexpr (S == STEPS - 1) ly.epi(ot, acc[o]);
+      });
+}
+#endif
 
 // bias-column operands of a layer: fragment g holds out tiles 4g..4g+3 (lanes 0-31)
 template <int OT>
@@ -396,7 +515,7 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
   {
     f32x16 q[2], sn[2];
     wfourier_q<DIM>(io, bt, 0, h, q);
-    run_steps<32, 4, 4, SITE_FWD_E0>(
+    run_steps<32, 4, WNL, SITE_FWD_E0>(
         ring, W, lane * 16, WE0Head{}, WHead{WF + OFF_EBLK * 4},
         [&](auto st, const f32x4 (&a)[4]) {
           constexpr int S = decltype(st)::value;
@@ -676,7 +795,7 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
   const int ntiles = (int)((a.n + WTILE - 1) / WTILE);
   const WScratch sc =
       make_wscratch(GRAD ? a.ws + (int64_t)slot * WSCRATCH_FLOATS_PER_WAVE : nullptr);
-  const Rsrc W = make_rsrc(a.P, PACKED_TOTAL * 4);
+  const Rsrc W = make_rsrc(a.P, (PNTF_WIDE_X6 ? PACKED_TOTAL_X6 : PACKED_TOTAL) * 4);
   __shared__ f32x4 wsig[GRAD ? WAVES * WL_TILES * 4 * 64 : 1];
   // each wave keeps its own copy of the head row (no workgroup barrier: a wave's LDS reads
   // follow its own writes in order)
@@ -740,6 +859,39 @@ __global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int co
   int n = 32 * ot + (l & 31);
   int k = 32 * kt + 8 * u + 4 * (l >> 5) + s;
   dst[o] = scale * (trans ? src[(int64_t)k * ld + n] : src[(int64_t)n * ld + k]);
+}
+
+// split-bf16 copy of the wide region's two directions (OFF_X6): step g = (matrix, ot, kt) of
+// the fp32 region (1024 floats: fragments u = 0..3) becomes fragments 3b + term of k block b,
+// whose element i is element i & 3 of fp32 fragment 2b + (i >> 2) of the same lane.
+__global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restrict__ x6) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (step, block, lane)
+  if (t >= (int64_t)(2 * SZ_DIR / 1024) * 2 * 64) return;
+  const int lane = (int)(t & 63), b = (int)((t >> 6) & 1);
+  const int gf = (int)(t >> 7);   // fp32 step: matrix base + ot·KT + kt
+  // the matrix (offset and shape in the direction's OFF_* order; Wᵀ in the second direction)
+  const int dir = gf >= SZ_DIR / 1024, f = gf * 1024 - dir * SZ_DIR;
+  int m0, out, in, nc;
+  if (f < OFF_EBLK) { m0 = OFF_E0; out = 128; in = 256; nc = 2; }
+  else if (f < OFF_GBLK) { m0 = OFF_EBLK + (f - OFF_EBLK) / SZ_E * SZ_E; out = in = 128; nc = 2; }
+  else if (f < OFF_G3) { m0 = OFF_GBLK + (f - OFF_GBLK) / SZ_G * SZ_G; out = in = 256; nc = 1; }
+  else { m0 = OFF_G3; out = 128; in = 256; nc = 1; }
+  if (dir) { const int x = out; out = in; in = x; }
+  const int OT = out / 32, KT = in / 32, G = wx6_group(OT, nc);
+  const int j = (f - m0) / 1024, ot = j / KT, kt = j % KT;
+  const int g = (gf - j) + (ot / G) * KT * G + kt * G + ot % G;   // x6 step index
+  const float* src = wide + (int64_t)gf * 1024;
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = src[((2 * b + (i >> 2)) * 64 + lane) * 4 + (i & 3)];
+  f32x16 tile;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tile[i] = v[i & 7];
+  wbf16x8 s[3];
+  wx6_split(tile, 0, s);
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    *reinterpret_cast<wbf16x8*>(x6 + (((int64_t)g * 6 + 3 * b + p) * 64 + lane) * 8) = s[p];
 }
 
 // bias columns, head vector and head bias of the wide region, from the plain bias block

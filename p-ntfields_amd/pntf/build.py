@@ -126,10 +126,11 @@ UNITS = (
     + [("fsplit_d%d_k%d" % (d, k), "pntf_kernels.hip",
         ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_SPLIT_FIELD"])
        for d in (3, 6) for k in range(5)]
-    # wide kernels (pntf_wide.h): a 2-step ring of 4 fragments (32-64 MFMAs of 64 cycles
-    # ahead)
+    # wide kernels (pntf_wide.h): a 2-step ring (32-64 fp32 MFMAs of 64 cycles ahead; 24-48
+    # bf16 MFMAs of 32 cycles in the split-bf16 layers, 6 fragments per step)
     + [("wide_d%d_k%d" % (d, k), "pntf_kernels.hip",
-        ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_WIDE_FIELD", "-DPNTF_PF_STEPS=2"])
+        ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_WIDE_FIELD", "-DPNTF_PF_STEPS=2",
+         "-DPNTF_WIDE_X6=1", "-DPNTF_RING_NL=6"])
        for d in (3, 6) for k in range(5)]
     # plan_kernel<6> holds the 6-dof path state beside the ring: a 2-step ring keeps it
     # spill-free (the 4-step ring spills 2 VGPRs there).

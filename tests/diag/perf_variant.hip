@@ -2,6 +2,7 @@
 // parameters (-DPNTF_PF_STEPS, -DPNTF_NO1).  Diagnostics only; built by
 // tests/diag/build_perf.sh into tests/diag/libperf_<name>.so and timed by perf_variants.py.
 #ifdef PERF_WIDE
+#define PNTF_UTIL   // pack_x6_kernel
 #include "pntf_wide.h"
 #elif defined(PERF_SPLIT)
 #include "pntf_split.h"
@@ -43,6 +44,21 @@ extern "C" int perf_tau_grad(int grid, const float* P, const float* xp, int64_t 
 #endif
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
+
+#ifdef PERF_WIDE
+// floats of the blob this build reads, and the split-bf16 region of an x6 build: P holds that
+// many floats, the first PACKED_TOTAL of them the production blob
+extern "C" long long perf_packed_total() {
+  return PNTF_WIDE_X6 ? pntf::PACKED_TOTAL_X6 : pntf::PACKED_TOTAL;
+}
+extern "C" int perf_pack_x6(float* P, hipStream_t stream) {
+  using namespace pntf;
+  const int64_t n = (int64_t)(2 * SZ_DIR / 1024) * 2 * 64;
+  hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     P + OFF_WIDE, reinterpret_cast<uint16_t*>(P + OFF_X6));
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+#endif
 
 #ifdef PNTF_DEBUG_DUMP
 extern "C" int perf_set_dbg(float* p) {

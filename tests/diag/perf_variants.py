@@ -67,16 +67,26 @@ def main(names):
     for name in names:
         if name.startswith("hsaco:"):
             fn = hsaco_launcher(os.path.join(ROOT, "tests", "diag", "hsaco_%s.hsaco" % name[6:]))
+            P = packed
         else:
             lib = ctypes.CDLL(os.path.join(ROOT, "tests", "diag", "libperf_%s.so" % name))
             fn = lib.perf_tau_grad
             fn.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_int64] + \
                 [ctypes.c_void_p] * 4 + [ctypes.c_void_p]
+            P = packed
+            if hasattr(lib, "perf_packed_total"):
+                lib.perf_packed_total.restype = ctypes.c_longlong
+                total = lib.perf_packed_total()
+                if total > packed.numel():   # x6 build: append the split-bf16 region
+                    P = torch.zeros(total, dtype=torch.float32, device=dev)
+                    P[:packed.numel()] = packed
+                    assert lib.perf_pack_x6(ctypes.c_void_p(P.data_ptr()),
+                                            ctypes.c_void_p(stream)) == 0
         t = torch.empty(n, device=dev)
         d = torch.empty(n, 6, device=dev)
 
         def run():
-            assert fn(grid, V(packed), V(xp), n, V(B), V(t), V(d), V(ws), stream) == 0
+            assert fn(grid, V(P), V(xp), n, V(B), V(t), V(d), V(ws), stream) == 0
         run()
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -84,6 +84,11 @@ __device__ __forceinline__ void wx6_split(const f32x16& v, int b, wbf16x8 (&s)[3
 #ifndef PNTF_X6_G1BUF
 #define PNTF_X6_G1BUF 1
 #endif
+#ifndef PNTF_X6_BM
+#define PNTF_X6_BM 1
+#endif
+// two-column layers in block-major steps (wlayer x6, pack_x6_kernel)
+constexpr bool wx6_block_major(int NC) { return PNTF_X6_BM && NC == 2; }
 constexpr int wx6_group(int OT, int NC) { return NC == 2 ? PNTF_X6_G2 : (OT < PNTF_X6_G1 ? OT : PNTF_X6_G1); }
 // the six products of order >= 2^-16, the small ones first
 __device__ __forceinline__ f32x16 wx6_mma(const f32x4& w0, const f32x4& w1, const f32x4& w2,
@@ -304,6 +309,38 @@ __device__ __forceinline__ void wlayer(Ring& ring, Rsrc W, int wbase, const f32x
                                        int lane, L& ly, PreF pre, NextF naddr) {
   static_assert(NC * KT <= 8 && NC * OT <= 8, "bank size");
   static_assert(NLN == 4, "the next step sequence's width comes from its head type");
+  if constexpr (wx6_block_major(NC)) {
+    // two-column layers (the encoder): step (g, kt, b) splits k block b of input tile kt once
+    // and runs it against the G = 2 out tiles of group g (fragments 3o + term), so a step
+    // holds one block's split (12 registers per column) and the split is shared by 2 tiles
+    constexpr int G = 2, STEPS = OT * KT;
+    static_assert(OT % G == 0 && 3 * G == 6, "block-major groups");
+    f32x16 acc[G][NC];
+    run_steps<STEPS, 6, wnext_nl<NextF>(), SITE>(
+        ring, W, lane * 16, WHead{wbase}, naddr, [&](auto st, const f32x4 (&a)[6]) {
+          constexpr int S = decltype(st)::value;
+          constexpr int g = S / (2 * KT), kt = (S / 2) % KT, b = S % 2;
+          if constexpr (S == 0) ly.start();
+          pre(st);
+          if constexpr (kt == 0 && b == 0) {
+#pragma unroll
+            for (int o = 0; o < G; ++o) ly.init(g * G + o, acc[o]);
+          }
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            wbf16x8 xs[3];
+            wx6_split<true>(in[c * KT + kt], b, xs);
+#pragma unroll
+            for (int o = 0; o < G; ++o)
+              acc[o][c] = wx6_mma(a[3 * o], a[3 * o + 1], a[3 * o + 2], xs, acc[o][c]);
+          }
+          if constexpr (kt == KT - 1 && b == 1) {
+#pragma unroll
+            for (int o = 0; o < G; ++o) ly.epi(g * G + o, acc[o]);
+          }
+        });
+    return;
+  }
   constexpr int G = wx6_group(OT, NC), STEPS = OT * KT;
   static_assert(OT % G == 0, "out tile groups");
   // accumulator buffers: one per tile of the group (G = 1 with PNTF_X6_G1BUF = 2: two,
@@ -877,9 +914,16 @@ __global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restr
   else if (f < OFF_G3) { m0 = OFF_GBLK + (f - OFF_GBLK) / SZ_G * SZ_G; out = in = 256; nc = 1; }
   else { m0 = OFF_G3; out = 128; in = 256; nc = 1; }
   if (dir) { const int x = out; out = in; in = x; }
-  const int OT = out / 32, KT = in / 32, G = wx6_group(OT, nc);
+  const int OT = out / 32, KT = in / 32;
   const int j = (f - m0) / 1024, ot = j / KT, kt = j % KT;
-  const int g = (gf - j) + (ot / G) * KT * G + kt * G + ot % G;   // x6 step index
+  // first fragment of (ot, kt, block b) in the x6 step order of wlayer; term p at + p
+  int64_t fr;
+  if (wx6_block_major(nc)) {   // step (g, kt, b), fragments 3o + p
+    fr = ((int64_t)(gf - j) + ((ot / 2) * KT + kt) * 2 + b) * 6 + (ot % 2) * 3;
+  } else {                     // step (g, kt, o), fragments 3b + p
+    const int G = wx6_group(OT, nc);
+    fr = ((int64_t)(gf - j) + (ot / G) * KT * G + kt * G + ot % G) * 6 + 3 * b;
+  }
   const float* src = wide + (int64_t)gf * 1024;
   float v[8];
 #pragma unroll
@@ -891,7 +935,7 @@ __global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restr
   wx6_split(tile, 0, s);
 #pragma unroll
   for (int p = 0; p < 3; ++p)
-    *reinterpret_cast<wbf16x8*>(x6 + (((int64_t)g * 6 + 3 * b + p) * 64 + lane) * 8) = s[p];
+    *reinterpret_cast<wbf16x8*>(x6 + ((fr + p) * 64 + lane) * 8) = s[p];
 }
 
 // bias columns, head vector and head bias of the wide region, from the plain bias block

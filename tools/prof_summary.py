@@ -59,6 +59,8 @@ def main():
     fetch_b = fetch["FETCH_SIZE"] * 1024 * 2
     write_b = write["WRITE_SIZE"] * 1024
     flops = mfma["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512
+    # the split-bf16 layers: six bf16 products per fp32 product
+    flops_bf16 = mfma.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512
     clock = mfma["GRBM_GUI_ACTIVE"] / 8 / (avg_ns * 1e-9) / 1e9
     simd_cycles = 1024 * avg_ns * 1e-9 * clock * 1e9
     j = {
@@ -69,7 +71,9 @@ def main():
         "hbm_bytes_per_launch": fetch_b + write_b,
         "hbm_bytes_per_pair": (fetch_b + write_b) / a.pairs,
         "hbm_GBps": (fetch_b + write_b) / (avg_ns * 1e-9) / 1e9,
-        "mfma_flops_per_launch": flops, "mfma_flops_per_pair": flops / a.pairs,
+        "mfma_flops_per_launch": flops, "mfma_flops_per_pair": flops / a.pairs,  # fp32 MFMA
+        "mfma_bf16_flops_per_launch": flops_bf16,
+        "mfma_fp32_equivalent_flops_per_pair": (flops + flops_bf16 / 6) / a.pairs,
         "mfma_busy_cycles": mfma["SQ_VALU_MFMA_BUSY_CYCLES"],
         "mfma_busy_frac_of_simd_cycles": mfma["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles,
         "effective_clock_GHz": clock, "sq_waves": mfma.get("SQ_WAVES"),

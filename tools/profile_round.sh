@@ -18,6 +18,6 @@ run() {  # run <dir> <seconds> <rocprofv3 args...>
 STEPS=20 run prof_stats 300 --kernel-trace --stats
 run pmc_fetch 300 --pmc FETCH_SIZE
 run pmc_write 300 --pmc WRITE_SIZE
-run pmc_mfma 300 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES
+run pmc_mfma 300 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
 run pmc_stall 300 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY

@@ -36,7 +36,7 @@ __global__ void copy_kernel(const float* __restrict__ src, int n, float* __restr
 __global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int cols, int ld,
                                  int trans, float scale, float* __restrict__ dst);
 __global__ void pack_wide_aux_kernel(const float* __restrict__ plain, float* __restrict__ wide);
-__global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restrict__ x6);
+__global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restrict__ x6, int bm);
 __global__ void pack_quad_kernel(const float* __restrict__ src, int rows, int cols, int dir,
                                  float* __restrict__ dst);
 __global__ void pack_quad_aux_kernel(const float* __restrict__ plain, float* __restrict__ quad);
@@ -376,8 +376,10 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
                      packed + OFF_BIAS, packed + OFF_QUAD);
   // the wide kernels' split-bf16 layers read a regrouped, pre-split copy of both directions
   const int64_t nx6 = (int64_t)(2 * SZ_DIR / 1024) * 2 * 64;
-  hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)((nx6 + 255) / 256)), dim3(256), 0, stream,
-                     packed + OFF_WIDE, reinterpret_cast<uint16_t*>(packed + OFF_X6));
+  for (int bm = 0; bm < 2; ++bm)
+    hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)((nx6 + 255) / 256)), dim3(256), 0, stream,
+                       packed + OFF_WIDE,
+                       reinterpret_cast<uint16_t*>(packed + (bm ? OFF_X6BM : OFF_X6)), bm);
   return check_launch("pack_weights");
 }
 

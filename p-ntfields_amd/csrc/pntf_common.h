@@ -105,7 +105,10 @@ constexpr int PACKED_TOTAL = OFF_QUAD + Q_SZ;
 // fp32 wide offset o sits at 1.5 o here)
 constexpr int OFF_X6 = (PACKED_TOTAL + 63) / 64 * 64;
 constexpr int X6_SZ = 3 * SZ_DIR;
-constexpr int PACKED_TOTAL_X6 = OFF_X6 + X6_SZ;
+// the same in block-major step order for the two-column (encoder) layers (pntf_wide.h
+// wx6_block_major; other layers' order is unchanged)
+constexpr int OFF_X6BM = OFF_X6 + X6_SZ;
+constexpr int PACKED_TOTAL_X6 = OFF_X6BM + X6_SZ;
 // Quad layer list in stream order: packed matrix (0..12, the OFF_* order above), direction
 // (0: A = W, 1: A = W^T), out rows, in features, plain bias offset (forward layers).
 struct QLayer {

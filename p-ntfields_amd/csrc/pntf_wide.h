@@ -85,10 +85,11 @@ __device__ __forceinline__ void wx6_split(const f32x16& v, int b, wbf16x8 (&s)[3
 #define PNTF_X6_G1BUF 1
 #endif
 #ifndef PNTF_X6_BM
-#define PNTF_X6_BM 1
+#define PNTF_X6_BM 0
 #endif
 // two-column layers in block-major steps (wlayer x6, pack_x6_kernel)
 constexpr bool wx6_block_major(int NC) { return PNTF_X6_BM && NC == 2; }
+// the order pack_x6_kernel writes: block-major for two-column layers into the OFF_X6BM copy
 constexpr int wx6_group(int OT, int NC) { return NC == 2 ? PNTF_X6_G2 : (OT < PNTF_X6_G1 ? OT : PNTF_X6_G1); }
 // the six products of order >= 2^-16, the small ones first
 __device__ __forceinline__ f32x16 wx6_mma(const f32x4& w0, const f32x4& w1, const f32x4& w2,
@@ -229,25 +230,47 @@ constexpr int WG4B = (OFF_WIDE + W_OFF_G4B) * 4;
 
 // standard layer: step st = ot·KT + kt reads fragments (ot, kt, u = l); base is the layer's
 // byte offset in the fp32 wide region.  x6: fragments (ot, kt, 3b + term) of the split copy
-struct WHead {
+// BMR: the block-major copy (OFF_X6BM) that two-column x6 layers read when PNTF_X6_BM
+template <bool BMR>
+struct WHeadT {
   int base;
   __device__ int operator()(int j, int l) const {
 #if PNTF_WIDE_X6
-    return OFF_X6 * 4 + (base - OFF_WIDE * 4) / 2 * 3 + (j * 6 + l) * 1024;
+    return (BMR ? OFF_X6BM : OFF_X6) * 4 + (base - OFF_WIDE * 4) / 2 * 3 + (j * 6 + l) * 1024;
 #else
     return base + (j * 4 + l) * 1024;
 #endif
   }
 };
+typedef WHeadT<false> WHead;
+typedef WHeadT<PNTF_WIDE_X6 && PNTF_X6_BM> WHeadE;   // an encoder layer (two columns)
 // fragments per step of whatever a step sequence hands over to (a WHead is always a wlayer)
+struct WE0Head;
 template <class F>
-constexpr int wnext_nl() { return std::is_same<F, WHead>::value ? WNL : 4; }
+constexpr int wnext_nl();
 // encoder[0] on Fourier features, k-tile outer: step st = kt·4 + ot (KT = 8)
+// x6 (PNTF_X6_E0): the split copy of encoder[0] (κ-scaled like its fp32 fragments), whose
+// two-column per-tile order is (ot·KT + kt) as well (PNTF_X6_G2 = 1)
+#ifndef PNTF_X6_E0
+#define PNTF_X6_E0 1
+#endif
+constexpr bool WE0X6 = PNTF_WIDE_X6 && PNTF_X6_E0;
+constexpr int WE0NL = WE0X6 ? 6 : 4;   // fragments per encoder[0] step
+static_assert(!WE0X6 || PNTF_X6_G2 == 1, "encoder[0]'s split copy in per-tile order");
 struct WE0Head {
   __device__ int operator()(int j, int l) const {
-    return WF + OFF_E0 * 4 + ((((j % 4) * 8 + j / 4) * 4 + l) * 1024);
+    if constexpr (WE0X6)
+      return OFF_X6 * 4 + (WF + OFF_E0 * 4 - OFF_WIDE * 4) / 2 * 3 +
+             ((((j % 4) * 8 + j / 4) * 6 + l) * 1024);
+    else
+      return WF + OFF_E0 * 4 + ((((j % 4) * 8 + j / 4) * 4 + l) * 1024);
   }
 };
+template <class F>
+constexpr int wnext_nl() {
+  if constexpr (std::is_same<F, WE0Head>::value) return WE0NL;
+  else return std::is_same<F, WHead>::value || std::is_same<F, WHeadE>::value ? WNL : 4;
+}
 // reverse sweep head: generator[-2]^T (OT 8, KT 4)
 __device__ __forceinline__ WHead wbwd_head() { return WHead{WB + OFF_G3 * 4}; }
 // Fourier fold (encoder[0]^T, OT 8, KT 4): step st = (o·4 + kt)·2 + half reads out tile
@@ -317,7 +340,7 @@ __device__ __forceinline__ void wlayer(Ring& ring, Rsrc W, int wbase, const f32x
     static_assert(OT % G == 0 && 3 * G == 6, "block-major groups");
     f32x16 acc[G][NC];
     run_steps<STEPS, 6, wnext_nl<NextF>(), SITE>(
-        ring, W, lane * 16, WHead{wbase}, naddr, [&](auto st, const f32x4 (&a)[6]) {
+        ring, W, lane * 16, WHeadE{wbase}, naddr, [&](auto st, const f32x4 (&a)[6]) {
           constexpr int S = decltype(st)::value;
           constexpr int g = S / (2 * KT), kt = (S / 2) % KT, b = S % 2;
           if constexpr (S == 0) ly.start();
@@ -552,9 +575,9 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
   {
     f32x16 q[2], sn[2];
     wfourier_q<DIM>(io, bt, 0, h, q);
-    run_steps<32, 4, WNL, SITE_FWD_E0>(
-        ring, W, lane * 16, WE0Head{}, WHead{WF + OFF_EBLK * 4},
-        [&](auto st, const f32x4 (&a)[4]) {
+    run_steps<32, WE0NL, WNL, SITE_FWD_E0>(
+        ring, W, lane * 16, WE0Head{}, WHeadE{WF + OFF_EBLK * 4},
+        [&](auto st, const f32x4 (&a)[WE0NL]) {
           constexpr int S = decltype(st)::value;
           constexpr int kt = S / 4, ot = S % 4;
           if constexpr (ot == 0 && kt < 4) {
@@ -572,17 +595,28 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
 #pragma unroll
             for (int c = 0; c < 2; ++c) X[c * 4 + ot] = mfma32(be0(ot), 1.f, zero16());
           }
+          if constexpr (WE0X6) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+            for (int c = 0; c < 2; ++c)
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-              for (int c = 0; c < 2; ++c) {
-                float b;
-                if constexpr (kt < 4) b = sn[c][4 * u + s];
-                else b = Y[c * 4 + kt - 4][4 * u + s];
-                X[c * 4 + ot] = mfma32(a[u][s], b, X[c * 4 + ot]);
+              for (int b = 0; b < 2; ++b) {
+                wbf16x8 xs[3];
+                wx6_split<true>(kt < 4 ? sn[c] : Y[c * 4 + (kt & 3)], b, xs);
+                X[c * 4 + ot] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs, X[c * 4 + ot]);
               }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                  float b;
+                  if constexpr (kt < 4) b = sn[c][4 * u + s];
+                  else b = Y[c * 4 + kt - 4][4 * u + s];
+                  X[c * 4 + ot] = mfma32(a[u][s], b, X[c * 4 + ot]);
+                }
+          }
           // next sin/cos tile's projections, after this tile's MFMAs are issued
           if constexpr (ot == 3 && kt < 3) wfourier_q<DIM>(io, bt, kt + 1, h, q);
           if constexpr (S == 16) a0bc.load(W, lane, B_EBLK);
@@ -614,16 +648,16 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
     a0.bc = a0bc;
     wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WE, X, lane, a0,
                                      at<0>([&] { b0.bc.load(W, lane, B_EBLK + 128); }),
-                                     WHead{WE + SZ_E * 4});
+                                     WHeadE{WE + SZ_E * 4});
     wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WE + SZ_E * 4, Y, lane, b0,
                                      at<0>([&] { a1.bc.load(W, lane, B_EBLK + 256); }),
-                                     WHead{WE + 2 * SZ_E * 4});
+                                     WHeadE{WE + 2 * SZ_E * 4});
     wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
                                      at<0>([&] { b1.bc.load(W, lane, B_EBLK + 384); }),
-                                     WHead{WE + 3 * SZ_E * 4});
+                                     WHeadE{WE + 3 * SZ_E * 4});
     wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
                                      at<0>([&] { e3.bc.load(W, lane, B_E3); }),
-                                     WHead{WF + OFF_E3 * 4});
+                                     WHeadE{WF + OFF_E3 * 4});
     // ---- encoder[-1] (:234) -> Y (zs = Y[0..3], zg = Y[4..7])
     wlayer<4, 4, 2, SITE_FWD_ENC, 4>(ring, W, WF + OFF_E3 * 4, X, lane, e3,
                                      at<0>([&] { gbc.load(W, lane, B_GBLK); }),
@@ -735,7 +769,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
                                      NoPre{}, WHead{WB + OFF_GBLK * 4});
     WBwd<8, 8, 1, true, false> la{X, sc, 0, lane};
     wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, WB + OFF_GBLK * 4, Y, lane, la, NoPre{},
-                                     WHead{WB + OFF_E3 * 4});
+                                     WHeadE{WB + OFF_E3 * 4});
   }
   // ---- merge Jacobian (:620-627): X[0..3] = dzs, X[4..7] = dzg
 #pragma unroll
@@ -751,16 +785,16 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
   {
     WBwd<4, 4, 2, false, true> e3{Y, sc, WT_EBLK + 24, lane};
     wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
-                                     WHead{WE + 3 * SZ_E * 4});
+                                     WHeadE{WE + 3 * SZ_E * 4});
     WBwd<4, 4, 2, false, true> b1{X, sc, WT_EBLK + 16, lane};
     wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, NoPre{},
-                                     WHead{WE + 2 * SZ_E * 4});
+                                     WHeadE{WE + 2 * SZ_E * 4});
     WBwd<4, 4, 2, true, true> a1{Y, sc, WT_EBLK + 8, lane};
     wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
-                                     WHead{WE + 1 * SZ_E * 4});
+                                     WHeadE{WE + 1 * SZ_E * 4});
     WBwd<4, 4, 2, false, true> b0{X, sc, WT_EBLK, lane};
     wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, NoPre{},
-                                     WHead{WE});
+                                     WHeadE{WE});
     WBwd<4, 4, 2, true, true> a0{Y, sc, WT_E0, lane};
     wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE, X, lane, a0, NoPre{}, WFoldHead{});
   }
@@ -773,7 +807,7 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
 #pragma unroll
   for (int d = 0; d < DIM; ++d) acc[0][d] = acc[1][d] = 0.f;
   f32x16 ph[2][2];   // [sin | cos rows][point]
-  run_steps<32, 4, 4, SITE_FOLD>(
+  run_steps<32, 4, wnext_nl<AfterF>(), SITE_FOLD>(
       ring, W, lane * 16, WFoldHead{}, after, [&](auto st, const f32x4 (&a)[4]) {
         constexpr int S = decltype(st)::value;
         constexpr int o = S / 8, kt = (S / 2) % 4, half = S % 2;
@@ -849,7 +883,7 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
       wbtab[i] = *reinterpret_cast<const f32x4*>(a.Btab + 4 * i);
   }
   Ring ring;
-  ring_fill<4>(ring, W, lane * 16, WE0Head{});
+  ring_fill<WE0NL>(ring, W, lane * 16, WE0Head{});
   if constexpr (BL) __syncthreads();
   for (int tile = slot; tile < ntiles; tile += nslots) {
     f32x16 X[8], Y[8];
@@ -901,7 +935,7 @@ __global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int co
 // split-bf16 copy of the wide region's two directions (OFF_X6): step g = (matrix, ot, kt) of
 // the fp32 region (1024 floats: fragments u = 0..3) becomes fragments 3b + term of k block b,
 // whose element i is element i & 3 of fp32 fragment 2b + (i >> 2) of the same lane.
-__global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restrict__ x6) {
+__global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restrict__ x6, int bm) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (step, block, lane)
   if (t >= (int64_t)(2 * SZ_DIR / 1024) * 2 * 64) return;
   const int lane = (int)(t & 63), b = (int)((t >> 6) & 1);
@@ -918,7 +952,7 @@ __global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restr
   const int j = (f - m0) / 1024, ot = j / KT, kt = j % KT;
   // first fragment of (ot, kt, block b) in the x6 step order of wlayer; term p at + p
   int64_t fr;
-  if (wx6_block_major(nc)) {   // step (g, kt, b), fragments 3o + p
+  if (bm && nc == 2) {   // step (g, kt, b), fragments 3o + p
     fr = ((int64_t)(gf - j) + ((ot / 2) * KT + kt) * 2 + b) * 6 + (ot % 2) * 3;
   } else {                     // step (g, kt, o), fragments 3b + p
     const int G = wx6_group(OT, nc);

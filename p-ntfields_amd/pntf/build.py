@@ -128,9 +128,11 @@ UNITS = (
        for d in (3, 6) for k in range(5)]
     # wide kernels (pntf_wide.h): a 2-step ring (32-64 fp32 MFMAs of 64 cycles ahead; 24-48
     # bf16 MFMAs of 32 cycles in the split-bf16 layers, 6 fragments per step)
+    # (block-major encoder layers, PNTF_X6_BM, where they stay spill-free: τ, travel time, and
+    # τ+∇τ at dim 3 — the headline)
     + [("wide_d%d_k%d" % (d, k), "pntf_kernels.hip",
         ["-DPNTF_DIM=%d" % d, "-DPNTF_KIND=%d" % k, "-DPNTF_WIDE_FIELD", "-DPNTF_PF_STEPS=2",
-         "-DPNTF_WIDE_X6=1", "-DPNTF_RING_NL=6"])
+         "-DPNTF_WIDE_X6=1", "-DPNTF_RING_NL=6", "-DPNTF_X6_BM=%d" % (k in (0, 4) or (d, k) == (3, 1))])
        for d in (3, 6) for k in range(5)]
     # plan_kernel<6> holds the 6-dof path state beside the ring: a 2-step ring keeps it
     # spill-free (the 4-step ring spills 2 VGPRs there).

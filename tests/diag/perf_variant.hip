@@ -54,8 +54,10 @@ extern "C" long long perf_packed_total() {
 extern "C" int perf_pack_x6(float* P, hipStream_t stream) {
   using namespace pntf;
   const int64_t n = (int64_t)(2 * SZ_DIR / 1024) * 2 * 64;
-  hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     P + OFF_WIDE, reinterpret_cast<uint16_t*>(P + OFF_X6));
+  for (int bm = 0; bm < 2; ++bm)
+    hipLaunchKernelGGL(pack_x6_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                       P + OFF_WIDE, reinterpret_cast<uint16_t*>(P + (bm ? OFF_X6BM : OFF_X6)),
+                       bm);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 #endif

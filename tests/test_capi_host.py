@@ -53,9 +53,10 @@ def test_pure_queries_without_gpu(lib):
     # then (64-float aligned) the quad streams: both directions once more, and per wave (8 per
     # quad workgroup) 14 bias / head fragments
     off_quad = (2 * mats + plain + wide + 63) // 64 * 64
-    # then (64-float aligned) the split-bf16 copy of the wide matrices: 3 bf16 terms per weight
+    # then (64-float aligned) two split-bf16 copies of the wide matrices (3 bf16 terms per
+    # weight; the second in block-major order for the encoder layers)
     off_x6 = (off_quad + 2 * mats + 8 * 14 * 256 + 63) // 64 * 64
-    assert lib.pntf_packed_floats() == off_x6 + 3 * mats
+    assert lib.pntf_packed_floats() == off_x6 + 2 * 3 * mats
     lib.pntf_status_string.restype = ctypes.c_char_p
     assert lib.pntf_status_string(1) == b"invalid argument"
 

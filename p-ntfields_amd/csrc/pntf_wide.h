@@ -246,6 +246,7 @@ typedef WHeadT<false> WHead;
 typedef WHeadT<PNTF_WIDE_X6 && PNTF_X6_BM> WHeadE;   // an encoder layer (two columns)
 // fragments per step of whatever a step sequence hands over to (a WHead is always a wlayer)
 struct WE0Head;
+struct WFoldHead;
 template <class F>
 constexpr int wnext_nl();
 // encoder[0] on Fourier features, k-tile outer: step st = kt·4 + ot (KT = 8)
@@ -266,21 +267,33 @@ struct WE0Head {
       return WF + OFF_E0 * 4 + ((((j % 4) * 8 + j / 4) * 4 + l) * 1024);
   }
 };
-template <class F>
-constexpr int wnext_nl() {
-  if constexpr (std::is_same<F, WE0Head>::value) return WE0NL;
-  else return std::is_same<F, WHead>::value || std::is_same<F, WHeadE>::value ? WNL : 4;
-}
 // reverse sweep head: generator[-2]^T (OT 8, KT 4)
 __device__ __forceinline__ WHead wbwd_head() { return WHead{WB + OFF_G3 * 4}; }
 // Fourier fold (encoder[0]^T, OT 8, KT 4): step st = (o·4 + kt)·2 + half reads out tile
 // o + 4·half (sin rows o, cos rows o + 4)
+// x6 (PNTF_X6_FOLD): the split copy of encoder[0]^T (per-tile order, as encoder[0]'s)
+#ifndef PNTF_X6_FOLD
+#define PNTF_X6_FOLD 0
+#endif
+constexpr bool WFX6 = PNTF_WIDE_X6 && PNTF_X6_FOLD;
+constexpr int WFNL = WFX6 ? 6 : 4;   // fragments per fold step
+static_assert(!WFX6 || PNTF_X6_G2 == 1, "encoder[0]^T's split copy in per-tile order");
 struct WFoldHead {
   __device__ int operator()(int j, int l) const {
     const int o = j / 8, kt = (j / 2) % 4, half = j % 2;
-    return WB + OFF_E0 * 4 + ((((o + 4 * half) * 4 + kt) * 4 + l) * 1024);
+    if constexpr (WFX6)
+      return OFF_X6 * 4 + (WB + OFF_E0 * 4 - OFF_WIDE * 4) / 2 * 3 +
+             ((((o + 4 * half) * 4 + kt) * 6 + l) * 1024);
+    else
+      return WB + OFF_E0 * 4 + ((((o + 4 * half) * 4 + kt) * 4 + l) * 1024);
   }
 };
+template <class F>
+constexpr int wnext_nl() {
+  if constexpr (std::is_same<F, WE0Head>::value) return WE0NL;
+  else if constexpr (std::is_same<F, WFoldHead>::value) return WFNL;
+  else return std::is_same<F, WHead>::value || std::is_same<F, WHeadE>::value ? WNL : 4;
+}
 
 // ---------------------------------------------------------------- generic wide layer
 #if !PNTF_WIDE_X6
@@ -807,21 +820,33 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
 #pragma unroll
   for (int d = 0; d < DIM; ++d) acc[0][d] = acc[1][d] = 0.f;
   f32x16 ph[2][2];   // [sin | cos rows][point]
-  run_steps<32, 4, wnext_nl<AfterF>(), SITE_FOLD>(
-      ring, W, lane * 16, WFoldHead{}, after, [&](auto st, const f32x4 (&a)[4]) {
+  run_steps<32, WFNL, wnext_nl<AfterF>(), SITE_FOLD>(
+      ring, W, lane * 16, WFoldHead{}, after, [&](auto st, const f32x4 (&a)[WFNL]) {
         constexpr int S = decltype(st)::value;
         constexpr int o = S / 8, kt = (S / 2) % 4, half = S % 2;
         if constexpr (kt == 0) {
 #pragma unroll
           for (int c = 0; c < 2; ++c) ph[half][c] = zero16();
         }
+        if constexpr (WFX6) {
+          // (split per step: keeping it for the second half spills)
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+          for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
+            for (int b = 0; b < 2; ++b) {
+              wbf16x8 xs[3];
+              wx6_split<true>(Y[c * 4 + kt], b, xs);
+              ph[half][c] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs, ph[half][c]);
+            }
+        } else {
 #pragma unroll
-            for (int c = 0; c < 2; ++c)
-              ph[half][c] = mfma32(a[u][s], Y[c * 4 + kt][4 * u + s], ph[half][c]);
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+              for (int c = 0; c < 2; ++c)
+                ph[half][c] = mfma32(a[u][s], Y[c * 4 + kt][4 * u + s], ph[half][c]);
+        }
         if constexpr (kt == 3 && half == 1) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {

@@ -1,0 +1,79 @@
+"""The split-bf16 copies of the wide weight fragments (pntf_wide.h pack_x6_kernel, DESIGN.md §3
+"split-bf16 layers"), read back from the packed blob and checked against their definition:
+
+  * every weight of the fp32 wide region (both directions, every matrix) appears once in each
+    copy, at the fragment the wide kernel's step order reads it from: per 32 x 32 step (ot, kt)
+    and k block b, element i of lane l holds M[32 ot + (l & 31)][32 kt + (i & 3) + 16 b +
+    8 (i >> 2) + 4 (l >> 5)], i.e. element i & 3 of fp32 fragment 2b + (i >> 2);
+  * step order: one-column layers (generator blocks, generator[-2]) in groups of 4 out tiles
+    (g, kt, o), fragments 3b + term; two-column layers (encoder[0], the encoder blocks,
+    encoder[-1]) per tile (ot, kt) in the first copy and block-major (g of 2 tiles, kt, b),
+    fragments 3o + term, in the second (OFF_X6BM);
+  * the three terms are the round-to-nearest-even bf16 splits x0 = bf16(x), x1 = bf16(x - x0),
+    x2 = bf16(x - x0 - x1), bit for bit, and x0 + x1 + x2 == x exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import weights
+from pntf import ops
+
+pytestmark = pytest.mark.gpu
+
+SZ_DIR = 128 * 256 + 4 * 128 * 128 + 128 * 128 + 6 * 256 * 256 + 128 * 256
+SZ_BIAS = 128 + 4 * 128 + 128 + 6 * 256 + 128 + 128 + 4
+# forward direction: (float offset, out, in, columns sharing the weights) in the OFF_* order
+MATS = ([(0, 128, 256, 2)] + [(32768 + 16384 * i, 128, 128, 2) for i in range(5)] +
+        [(114688 + 65536 * i, 256, 256, 1) for i in range(6)] + [(507904, 128, 256, 1)])
+
+
+def bf16_rne(x):
+    """float32 -> the float32 value of its round-to-nearest-even bf16 (finite inputs)."""
+    u = x.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return (r & 0xFFFFFFFF).astype(np.uint32).view(np.float32)
+
+
+def frag_index(gf, j, OT, KT, nc, b, bm):
+    ot, kt = divmod(j, KT)
+    base = gf - j
+    if nc == 2 and bm:
+        return (base + ((ot // 2) * KT + kt) * 2 + b) * 6 + (ot % 2) * 3
+    G = 1 if nc == 2 else 4
+    return (base + (ot // G) * KT * G + kt * G + ot % G) * 6 + 3 * b
+
+
+def test_x6_copies_match_their_definition():
+    dev = torch.device("cuda:0")
+    packed = ops.pack_weights([torch.from_numpy(v).to(dev) for v in weights().values()])
+    P = packed.cpu().numpy()
+    x6_sz = 3 * SZ_DIR
+    off_bm = P.size - x6_sz
+    off_x6 = off_bm - x6_sz
+    off_wide = 2 * SZ_DIR + SZ_BIAS
+    wide = P[off_wide:off_wide + 2 * SZ_DIR].reshape(-1, 4, 64, 4)     # step, u, lane, s
+    # fp32 values of (step, block, lane, i): element i & 3 of fragment 2b + (i >> 2)
+    vals = wide.reshape(-1, 2, 2, 64, 4).transpose(0, 1, 3, 2, 4).reshape(-1, 2, 64, 8)
+    x0 = bf16_rne(vals)
+    x1 = bf16_rne(vals - x0)
+    x2 = bf16_rne(vals - x0 - x1)
+    assert np.array_equal(x0.astype(np.float64) + x1 + x2, vals.astype(np.float64))
+    want = np.stack([x0, x1, x2], axis=2)                              # step, b, term, lane, i
+    for off, bm in ((off_x6, False), (off_bm, True)):
+        bits = P[off:off + x6_sz].view(np.uint16).reshape(-1, 64, 8).astype(np.uint32) << 16
+        got = bits.view(np.float32)                                   # fragment, lane, i
+        seen = np.zeros(got.shape[0], dtype=np.int32)
+        for d in (0, 1):
+            for m0, out, inn, nc in MATS:
+                if d:
+                    out, inn = inn, out
+                OT, KT = out // 32, inn // 32
+                for j in range(OT * KT):
+                    gf = (d * SZ_DIR + m0) // 1024 + j
+                    for b in range(2):
+                        fr = frag_index(gf, j, OT, KT, nc, b, bm)
+                        for p in range(3):
+                            assert np.array_equal(got[fr + p], want[gf, b, p]), (d, m0, j, b, p, bm)
+                            seen[fr + p] += 1
+        assert (seen == 1).all(), "every fragment written once"

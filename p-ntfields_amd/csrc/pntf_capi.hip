@@ -37,6 +37,8 @@ __global__ void pack_wide_kernel(const float* __restrict__ src, int rows, int co
                                  int trans, float scale, float* __restrict__ dst);
 __global__ void pack_wide_aux_kernel(const float* __restrict__ plain, float* __restrict__ wide);
 __global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restrict__ x6, int bm);
+__global__ void pack_nx6_kernel(const float* __restrict__ src, int rows, int cols,
+                                uint16_t* __restrict__ dst);
 __global__ void pack_quad_kernel(const float* __restrict__ src, int rows, int cols, int dir,
                                  float* __restrict__ dst);
 __global__ void pack_quad_aux_kernel(const float* __restrict__ plain, float* __restrict__ quad);
@@ -287,7 +289,7 @@ const char* pntf_status_string(int status) {
 
 const char* pntf_last_error(void) { return g_err; }
 
-size_t pntf_packed_floats(void) { return (size_t)PACKED_TOTAL_X6; }
+size_t pntf_packed_floats(void) { return (size_t)PACKED_TOTAL_NX6; }
 
 const char* pntf_build_info(void) { return PNTF_BUILD_INFO; }
 
@@ -334,7 +336,7 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
       {28, 256, 256, OFF_GBLK + 5 * SZ_G},                    // generator1.2
       {20, 128, 256, OFF_G3},                                 // generator.3
   };
-  hipMemsetAsync(packed, 0, sizeof(float) * PACKED_TOTAL_X6, stream);
+  hipMemsetAsync(packed, 0, sizeof(float) * PACKED_TOTAL_NX6, stream);
   for (int m = 0; m < (int)(sizeof(mats) / sizeof(mats[0])); ++m) {
     const M& d = mats[m];
     int64_t cnt = (int64_t)d.rows * d.cols;
@@ -351,6 +353,10 @@ int pntf_pack_weights(const float* const* params, int n_params, float* packed,
                        packed + OFF_WIDE + OFF_FWD + d.off);
     hipLaunchKernelGGL(pack_wide_kernel, dim3(blocks), dim3(256), 0, stream, params[d.idx],
                        d.cols, d.rows, d.cols, 1, 1.f, packed + OFF_WIDE + OFF_BWD + d.off);
+    // the residual kernel's split-bf16 Taylor layers (16x16x32 step order, forward only)
+    hipLaunchKernelGGL(pack_nx6_kernel, dim3((unsigned)((cnt / 8 + 255) / 256)), dim3(256), 0,
+                       stream, params[d.idx], d.rows, d.cols,
+                       reinterpret_cast<uint16_t*>(packed + OFF_NX6 + d.off / 2 * 3));
   }
   // the quad streams: every layer of both directions in planner-step order
   for (int L = 0; L < Q_NL; ++L) {
@@ -390,7 +396,7 @@ struct pntf_net {
 
 pntf_net* pntf_net_create(const float* const* params, int n_params, hipStream_t stream) {
   float* p = nullptr;
-  if (hipMalloc(&p, sizeof(float) * PACKED_TOTAL_X6) != hipSuccess) {
+  if (hipMalloc(&p, sizeof(float) * PACKED_TOTAL_NX6) != hipSuccess) {
     fail(PNTF_ERR_HIP, "pntf_net_create: hipMalloc of the packed weights failed%s");
     return nullptr;
   }

@@ -51,10 +51,132 @@ struct TaylorL {
   }
 };
 
+// ---------------------------------------------------------------- split-bf16 Taylor layers
+// PNTF_TAYLOR_X6 = 1 (round 6): the direction passes' encoder / generator layers run each fp32
+// product as six v_mfma_f32_16x16x32_bf16 on three-term bf16 splits of both operands (the
+// headline's and the training GEMMs' scheme: x = x0 + x1 + x2 exactly, the three products of
+// order < 2^-16 dropped, fp32 accumulation): 6 x 16 cycles where the fp32 step took 8 x 32.
+// The activation layout is unchanged: for the 16x16x32 B operand lane (t, g) supplies k =
+// 8 g + i, i.e. rows 4 g .. 4 g + 3 of input tiles 2 b (i < 4) and 2 b + 1 (i >= 4) — its own
+// registers — and the weights are pre-split in that k order (OFF_NX6, pack_nx6_kernel).
+#ifndef PNTF_TAYLOR_X6
+#define PNTF_TAYLOR_X6 1
+#endif
+typedef __bf16 nbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 nbf16x2 __attribute__((ext_vector_type(2)));
+typedef float nf32x2 __attribute__((ext_vector_type(2)));
+// three-term RNE split of the 8 k values (lo: rows of tile 2b, hi: of tile 2b + 1)
+__device__ __forceinline__ void nx6_split(const f32x4& lo, const f32x4& hi, nbf16x8 (&s)[3]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    nf32x2 x = i < 2 ? nf32x2{lo[2 * i], lo[2 * i + 1]} : nf32x2{hi[2 * i - 4], hi[2 * i - 3]};
+    asm volatile("" : "+v"(x));   // split here, not hoisted into a whole split bank
+    const nbf16x2 p0 = __builtin_convertvector(x, nbf16x2);
+    const nf32x2 r1 = x - __builtin_convertvector(p0, nf32x2);
+    const nbf16x2 p1 = __builtin_convertvector(r1, nbf16x2);
+    const nf32x2 r2 = r1 - __builtin_convertvector(p1, nf32x2);
+    const nbf16x2 p2 = __builtin_convertvector(r2, nbf16x2);
+    s[0][2 * i] = p0[0]; s[0][2 * i + 1] = p0[1];
+    s[1][2 * i] = p1[0]; s[1][2 * i + 1] = p1[1];
+    s[2][2 * i] = p2[0]; s[2][2 * i + 1] = p2[1];
+  }
+}
+// the six products of order >= 2^-16, the small ones first
+__device__ __forceinline__ f32x4 nx6_mma(const f32x4& w0, const f32x4& w1, const f32x4& w2,
+                                         const nbf16x8 (&x)[3], f32x4 acc) {
+  const nbf16x8 a0 = __builtin_bit_cast(nbf16x8, w0), a1 = __builtin_bit_cast(nbf16x8, w1),
+                a2 = __builtin_bit_cast(nbf16x8, w2);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, x[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, x[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, x[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x[0], acc, 0, 0, 0);
+}
+// out tiles of a group (one split of each input block per group)
+template <int OT>
+constexpr int nx6_group() { return OT < NX6_G ? OT : NX6_G; }
+
+// (J, L) <- [act](A·(J, L) (+ residual)) as TaylorL, on split-bf16 MFMA.  Step (g, b, o) runs
+// k block b (input tiles 2b, 2b + 1) of out tile g·G + o for both columns; the block is split
+// at o = 0 and shared by the G tiles of the group.  A tile's σ tile is loaded when it starts
+// (b = 0, NB steps of G before its epilogue) and the epilogue runs at its last step.
+// wbase: the layer's byte offset in the forward fp32 direction (its split copy sits at 1.5x).
+template <int OT, int KT, bool RES, bool ACT, int NIN, int NOUT>
+__device__ __forceinline__ void taylor_layer_x6(Rsrc W, int wbase, const f32x4 (&in)[NIN],
+                                                f32x4 (&out)[NOUT], Scratch sc, int sig0,
+                                                int lane) {
+  constexpr int NB = KT / 2, G = nx6_group<OT>(), STEPS = OT * NB;
+  static_assert(KT % 2 == 0 && OT % G == 0 && 2 * KT <= NIN && 2 * OT <= NOUT, "layer shape");
+  const int base = OFF_NX6 * 4 + wbase / 2 * 3;
+  auto addr = [&](int st, int l) { return base + (st * 3 + l) * 1024; };
+  Ring ring;
+  ring_fill<3>(ring, W, lane * 16, addr);
+  f32x4 acc[G][2], gs[G];
+  nbf16x8 xs[2][3];
+  run_steps<STEPS, 3, 0, SITE_TAYLOR>(
+      ring, W, lane * 16, addr, NoNext{}, [&](auto st, const f32x4 (&a)[3]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int o = S % G, b = (S / G) % NB, ot = (S / (G * NB)) * G + o;
+        if constexpr (o == 0) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) nx6_split(in[c * KT + 2 * b], in[c * KT + 2 * b + 1], xs[c]);
+        }
+        if constexpr (b == 0) {
+          if (ACT) gs[o] = load_tile(sc, sig0 + ot, lane);
+#pragma unroll
+          for (int c = 0; c < 2; ++c) acc[o][c] = RES ? out[c * OT + ot] : zero4();
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[o][c] = nx6_mma(a[0], a[1], a[2], xs[c], acc[o][c]);
+        if constexpr (b == NB - 1) {
+          if (!ACT) {
+            out[ot] = acc[o][0];
+            out[OT + ot] = acc[o][1];
+          } else {
+            const f32x4 gg = gs[o], J = acc[o][0], L = acc[o][1];
+            out[ot] = gg * J;                                                // :686
+            out[OT + ot] = (10.f * gg * (1.f - gg)) * J * J + gg * L;        // :682-684
+          }
+        }
+      });
+}
+
+#if defined(PNTF_UTIL)
+// Narrow split-bf16 copy of one forward matrix M (rows x cols, row-major; OFF_NX6): step
+// st = (g·NB + b)·G + o of taylor_layer_x6 holds, for out tile ot = g·G + o and k block b, the
+// three RNE bf16 terms of A[r][k] = M[16 ot + r][16 (2b + (i >> 2)) + 4 q + (i & 3)] at lane
+// l = (r, q) = (l & 15, l >> 4), element i = k - 8 q; fragment 3 st + term, 1 KiB each.
+__global__ void pack_nx6_kernel(const float* __restrict__ src, int rows, int cols,
+                                uint16_t* __restrict__ dst) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;   // (step, lane)
+  const int OT = rows / 16, NB = cols / 32, G = OT < NX6_G ? OT : NX6_G;
+  if (t >= OT * NB * 64) return;
+  const int l = t & 63, st = t >> 6;
+  const int o = st % G, b = (st / G) % NB, ot = (st / (G * NB)) * G + o;
+  const int r = l & 15, q = l >> 4;
+  f32x4 lo, hi;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    lo[i] = src[(int64_t)(16 * ot + r) * cols + 16 * (2 * b) + 4 * q + i];
+    hi[i] = src[(int64_t)(16 * ot + r) * cols + 16 * (2 * b + 1) + 4 * q + i];
+  }
+  nbf16x8 s[3];
+  nx6_split(lo, hi, s);
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    *reinterpret_cast<nbf16x8*>(dst + ((int64_t)(st * 3 + p) * 64 + l) * 8) = s[p];
+}
+#endif  // PNTF_UTIL
+
 template <int OT, int KT, bool RES, bool ACT, int NIN, int NOUT>
 __device__ __forceinline__ void taylor_layer(Rsrc W, int wbase, const f32x4 (&in)[NIN],
                                              f32x4 (&out)[NOUT], Scratch sc, int sig0,
                                              int lane) {
+  if constexpr (PNTF_TAYLOR_X6) {
+    taylor_layer_x6<OT, KT, RES, ACT>(W, wbase, in, out, sc, sig0, lane);
+    return;
+  }
   TaylorL<OT, KT, RES, ACT, NOUT> ly{out, sc, sig0, lane};
   Ring ring;
   ring_fill<2>(ring, W, lane * 16, Head<KT, 2>{wbase});
@@ -186,7 +308,8 @@ __device__ __forceinline__ void residual_body(const ResidualArgs& a, int slot, i
   const int lane = threadIdx.x & 63;
   const int64_t ntiles = (a.n + TILE - 1) / TILE;
   const Scratch sc = make_scratch(a.ws + (int64_t)slot * SCRATCH_FLOATS_PER_WAVE);
-  const Rsrc W = make_rsrc(a.P, PACKED_FLOATS * 4);
+  // the whole blob: the split-bf16 Taylor layers read the OFF_NX6 copy
+  const Rsrc W = make_rsrc(a.P, PACKED_TOTAL_NX6 * 4);
   const float nan = __builtin_nanf("");
   for (int64_t tile = slot; tile < ntiles; tile += nslots) {
     const int64_t pair = tile * TILE + (lane & 15);

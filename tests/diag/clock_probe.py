@@ -55,7 +55,7 @@ def soak(fn, seconds=2.0):
     return a.elapsed_time(b)
 
 
-def main():
+def main(only=None, wlib="libperf_wstamp.so"):
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -64,7 +64,7 @@ def main():
     packed = ops.pack_weights([torch.from_numpy(W[k]).to(dev) for k in synth.state_dict_keys()])
     out = {}
     # ---- headline wide kernel (1M pairs)
-    lib = ctypes.CDLL(os.path.join(HERE, "libperf_wstamp.so"))
+    lib = ctypes.CDLL(os.path.join(HERE, wlib))
     n = 1 << 20
     xp = torch.from_numpy(synth.make_pairs(n, 3, seed=1000)).to(dev)
     B = torch.from_numpy(synth.make_B(3, seed=1)).to(dev).unsqueeze(0).contiguous()
@@ -75,7 +75,9 @@ def main():
     ms = soak(lambda: lib.perf_tau_grad(cus, V(packed), V(xp), n, V(B), V(t), V(d), V(ws),
                                         stream))
     out["wide_tau_grad_1M"] = dict(clocks(lib, cus), launch_ms=ms)
-    print(json.dumps({"wide_tau_grad_1M": out["wide_tau_grad_1M"]}), flush=True)
+    print(json.dumps({"wide_tau_grad_1M": out["wide_tau_grad_1M"], "lib": wlib}), flush=True)
+    if only == "wide":
+        return
     # ---- C5 planner, quad MFMA tiles only (no tail hand-off)
     lib = ctypes.CDLL(os.path.join(HERE, "libperf_qstamp.so"))
     q = 1024
@@ -127,4 +129,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    # python tests/diag/clock_probe.py [wide [libperf_<name>.so]]: the headline leg only
+    main(*sys.argv[1:])

@@ -56,7 +56,9 @@ def test_pure_queries_without_gpu(lib):
     # then (64-float aligned) two split-bf16 copies of the wide matrices (3 bf16 terms per
     # weight; the second in block-major order for the encoder layers)
     off_x6 = (off_quad + 2 * mats + 8 * 14 * 256 + 63) // 64 * 64
-    assert lib.pntf_packed_floats() == off_x6 + 2 * 3 * mats
+    # then the forward matrices split for the residual kernel's 16x16x32 Taylor layers
+    off_nx6 = (off_x6 + 2 * 3 * mats + 63) // 64 * 64
+    assert lib.pntf_packed_floats() == off_nx6 + 3 * mats // 2
     lib.pntf_status_string.restype = ctypes.c_char_p
     assert lib.pntf_status_string(1) == b"invalid argument"
 

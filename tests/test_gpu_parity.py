@@ -421,6 +421,15 @@ def test_residual_grad_agrees_with_reverse_sweep(packed, dev, W):
     dd = np.abs(got["diff"].astype(np.float64) - dfo) / (np.abs(dfo) + 4.0)
     print("C3 diff |err|/(|diff|+4) max %.2e" % dd.max())
     assert dd.max() < 1e-4
+    # componentwise (floored at 1 % of the largest component), ∇τ and Δτ: the direction passes
+    # run on split-bf16 MFMA (pntf_taylor.h, round 6) and must be no worse than the fp32 op
+    # sequence of out_laplace (the oracle in float32) against the same fp64 values
+    _, do32, lo32 = O.laplace(W, xp_np[idx], Bt_np, env_np[idx], dim=3, dtype=np.float32)
+    for k, ref64, ref32 in (("dtau", do, do32), ("ltau", lo, lo32)):
+        floor = ELEM_FLOOR * np.abs(ref64).max()
+        e_hip, e_ref = max_rel(got[k], ref64, floor), max_rel(ref32, ref64, floor)
+        print("C3 %s componentwise vs fp64: HIP %.2e, fp32 op sequence %.2e" % (k, e_hip, e_ref))
+        assert e_hip <= max(1e-4, e_ref), k
     # the 16-pair τ+∇τ kernel runs the same forward MFMA sequence: τ bit-identical
     t, d = ops.tau_grad(packed, xp, Bt, env, dim=3, schedule="wave_tile")
     assert torch.equal(out["tau"], t)
@@ -622,3 +631,61 @@ def test_net_handle_matches_packed_blob(packed, dev, W):
         torch.cuda.synchronize()
         lib.pntf_net_destroy(h)
     assert not lib.pntf_net_create(None, 30, s) and b"null" in lib.pntf_last_error()
+
+
+def test_hip_graph_capture_through_the_abi(packed, dev, W):
+    """The C ABI is stream-ordered: pntf_tau_grad and pntf_eikonal_residual
+    launched through ctypes on torch's capture stream are recorded into a torch.cuda.CUDAGraph
+    (hipStreamBeginCapture / EndCapture) and every replay, on new inputs copied into the static
+    buffers, is bitwise the eager call on the same inputs.  (Round 5's capture segfault in
+    hipStreamEndCapture: DESIGN.md §7 item 7.)"""
+    import ctypes
+    from pntf import _lib
+    lib = _lib.load()
+    V = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
+    n, E = 40000, 10
+    Bt = T(synth.make_B_table(E, 3), dev)
+    ws = torch.empty(int(lib.pntf_workspace_bytes(n)), dtype=torch.uint8, device=dev)
+
+    def inputs(seed):
+        return (T(synth.make_pairs(n, 3, seed=seed), dev),
+                T(synth.make_env_ids(n, E, contiguous=False, seed=seed), dev, torch.int32),
+                T(synth.make_speeds(n, seed=seed), dev))
+
+    def outputs():
+        return [torch.empty(n, device=dev), torch.empty((n, 6), device=dev),
+                torch.empty(n, device=dev), torch.empty((n, 6), device=dev),
+                torch.empty((n, 6), device=dev), torch.empty(n, device=dev)]
+
+    def launch(x, e, y, o):
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        st = lib.pntf_tau_grad(V(packed), 3, V(x), n, V(Bt), V(e), E, 0, V(o[0]), V(o[1]),
+                               V(ws), ws.numel(), s)
+        assert st == 0, lib.pntf_last_error()
+        st = lib.pntf_eikonal_residual(V(packed), 3, V(x), V(y), n, V(Bt), V(e), E,
+                                       ctypes.c_float(1e-3), V(o[2]), V(o[3]), V(o[4]),
+                                       V(o[5]), V(ws), ws.numel(), s)
+        assert st == 0, lib.pntf_last_error()
+
+    xs, es, ys = [t.clone() for t in inputs(11)]
+    go = outputs()
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        launch(xs, es, ys, go)                   # warm-up on the side stream
+    torch.cuda.current_stream(dev).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        launch(xs, es, ys, go)
+    for seed in (12, 13):
+        x, e, y = inputs(seed)
+        xs.copy_(x), es.copy_(e), ys.copy_(y)
+        g.replay()
+        ref = outputs()
+        launch(x, e, y, ref)
+        torch.cuda.synchronize()
+        for a, b in zip(go, ref):
+            assert torch.equal(a, b)
+    # and the replayed τ+∇τ is the one the ops wrapper gives (same kernel, same inputs)
+    t, d = ops.tau_grad(packed, x, Bt, e, dim=3)
+    assert torch.equal(t, go[0]) and torch.equal(d, go[1])

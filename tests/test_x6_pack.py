@@ -24,6 +24,12 @@ pytestmark = pytest.mark.gpu
 SZ_DIR = 128 * 256 + 4 * 128 * 128 + 128 * 128 + 6 * 256 * 256 + 128 * 256
 SZ_BIAS = 128 + 4 * 128 + 128 + 6 * 256 + 128 + 128 + 4
 # forward direction: (float offset, out, in, columns sharing the weights) in the OFF_* order
+# the narrow (16x16x32) split copy of the forward direction (pntf_taylor.h pack_nx6_kernel)
+NX6_SZ = 3 * SZ_DIR // 2
+NX6_G = 8
+NAMES = ["encoder.0", "encoder.1", "encoder1.1", "encoder.2", "encoder1.2", "encoder.3",
+         "generator.0", "generator1.0", "generator.1", "generator1.1", "generator.2",
+         "generator1.2", "generator.3"]
 MATS = ([(0, 128, 256, 2)] + [(32768 + 16384 * i, 128, 128, 2) for i in range(5)] +
         [(114688 + 65536 * i, 256, 256, 1) for i in range(6)] + [(507904, 128, 256, 1)])
 
@@ -49,7 +55,7 @@ def test_x6_copies_match_their_definition():
     packed = ops.pack_weights([torch.from_numpy(v).to(dev) for v in weights().values()])
     P = packed.cpu().numpy()
     x6_sz = 3 * SZ_DIR
-    off_bm = P.size - x6_sz
+    off_bm = P.size - NX6_SZ - x6_sz      # the narrow split copy (round 6) comes last
     off_x6 = off_bm - x6_sz
     off_wide = 2 * SZ_DIR + SZ_BIAS
     wide = P[off_wide:off_wide + 2 * SZ_DIR].reshape(-1, 4, 64, 4)     # step, u, lane, s
@@ -77,3 +83,43 @@ def test_x6_copies_match_their_definition():
                             assert np.array_equal(got[fr + p], want[gf, b, p]), (d, m0, j, b, p, bm)
                             seen[fr + p] += 1
         assert (seen == 1).all(), "every fragment written once"
+
+
+def test_nx6_copy_matches_its_definition():
+    """The residual kernel's split-bf16 Taylor layers (pntf_taylor.h taylor_layer_x6, round 6)
+    read the forward matrices pre-split for v_mfma_f32_16x16x32_bf16: step st = (g·NB + b)·G + o
+    (out tile ot = g·G + o of 16 rows, k block b of 32 features, G = min(OT, 8)) holds at lane
+    l = (r, q) = (l & 15, l >> 4), element i, the three RNE bf16 terms of
+    M[16 ot + r][16 (2b + (i >> 2)) + 4 q + (i & 3)], fragment 3 st + term; a matrix at forward
+    offset o starts at 1.5 o."""
+    dev = torch.device("cuda:0")
+    W = weights()
+    packed = ops.pack_weights([torch.from_numpy(v).to(dev) for v in W.values()])
+    P = packed.cpu().numpy()
+    nx6 = P[P.size - NX6_SZ:]
+    seen = 0
+    for (m0, out, inn, _), name in zip(MATS, NAMES):
+        M = np.asarray(W[name + ".weight"], np.float32)
+        assert M.shape == (out, inn)
+        OT, NB = out // 16, inn // 32
+        G = min(OT, NX6_G)
+        st = np.arange(OT * NB)
+        o, b, ot = st % G, (st // G) % NB, (st // (G * NB)) * G + st % G
+        lane, i = np.arange(64), np.arange(8)
+        r, q = lane & 15, lane >> 4
+        rows = 16 * ot[:, None, None] + r[None, :, None]
+        cols = 16 * (2 * b[:, None, None] + (i[None, None, :] >> 2)) + 4 * q[None, :, None] + \
+            (i[None, None, :] & 3)
+        vals = M[rows, cols]                                              # step, lane, i
+        x0 = bf16_rne(vals)
+        x1 = bf16_rne(vals - x0)
+        x2 = bf16_rne(vals - x0 - x1)
+        assert np.array_equal(x0.astype(np.float64) + x1 + x2, vals.astype(np.float64))
+        off = m0 * 3 // 2
+        n = OT * NB * 3 * 256                          # floats of the copy (1 KiB fragments)
+        bits = nx6[off:off + n].view(np.uint16).reshape(OT * NB, 3, 64, 8).astype(np.uint32)
+        got = (bits << 16).view(np.float32)
+        for p, want in enumerate((x0, x1, x2)):
+            assert np.array_equal(got[:, p], want), (name, p)
+        seen += n
+    assert seen == NX6_SZ

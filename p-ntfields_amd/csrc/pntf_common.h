@@ -112,9 +112,10 @@ constexpr int PACKED_TOTAL_X6 = OFF_X6BM + X6_SZ;
 // Split-bf16 narrow fragments (pntf_taylor.h, the residual kernel's Taylor directions on
 // v_mfma_f32_16x16x32_bf16, round 6): the forward direction regrouped per (16-row out tile,
 // 32-feature k block) into 3 bf16 terms of 1 KiB each, in taylor_layer_x6's step order (out
-// tiles in groups of NX6_G sharing one split of the input block); a matrix at forward offset o
+// tiles in groups of NX6_G sharing one split of the input block: 16 = every layer's out tiles
+// in one group, the residual kernel accumulating in its out bank); a matrix at forward offset o
 // sits at 1.5 o here.
-constexpr int NX6_G = 8;
+constexpr int NX6_G = 16;
 constexpr int OFF_NX6 = (PACKED_TOTAL_X6 + 63) / 64 * 64;
 constexpr int NX6_SZ = 3 * SZ_DIR / 2;
 constexpr int PACKED_TOTAL_NX6 = OFF_NX6 + NX6_SZ;

@@ -62,6 +62,10 @@ struct TaylorL {
 #ifndef PNTF_TAYLOR_X6
 #define PNTF_TAYLOR_X6 1
 #endif
+// accumulate in the out bank, every out tile in one group (NX6_G = 16, pntf_common.h)
+#ifndef PNTF_TAYLOR_ACC
+#define PNTF_TAYLOR_ACC 1
+#endif
 typedef __bf16 nbf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 nbf16x2 __attribute__((ext_vector_type(2)));
 typedef float nf32x2 __attribute__((ext_vector_type(2)));
@@ -112,6 +116,44 @@ __device__ __forceinline__ void taylor_layer_x6(Rsrc W, int wbase, const f32x4 (
   auto addr = [&](int st, int l) { return base + (st * 3 + l) * 1024; };
   Ring ring;
   ring_fill<3>(ring, W, lane * 16, addr);
+#if PNTF_TAYLOR_ACC
+  // the out bank is the accumulator (residual: its initial value), so the G = OT out tiles
+  // share each input block's split (NX6_G covers every layer); tile ot's act epilogue runs
+  // right after its last block's MFMAs
+  {
+    nbf16x8 xs[2][3];
+    // σ tile of out tile t: loaded TSD steps before its epilogue (step (NB-1)·OT + t) into a
+    // ring of TSD + 1 slots (a whole layer's σ tiles at once spilled in the dim-6 unit)
+    constexpr int TSD = OT < 8 ? OT : 8, NGS = TSD + 1;
+    f32x4 gs[NGS];
+    run_steps<STEPS, 3, 0, SITE_TAYLOR>(
+        ring, W, lane * 16, addr, NoNext{}, [&](auto st, const f32x4 (&a)[3]) {
+          constexpr int S = decltype(st)::value;
+          constexpr int o = S % G, b = (S / G) % NB, ot = (S / (G * NB)) * G + o;
+          static_assert(G == OT, "one group");
+          constexpr int LT = S + TSD - (NB - 1) * OT;   // the tile whose σ loads at this step
+          if constexpr (ACT && LT >= 0 && LT < OT) gs[LT % NGS] = load_tile(sc, sig0 + LT, lane);
+          if constexpr (o == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+              nx6_split(in[c * KT + 2 * b], in[c * KT + 2 * b + 1], xs[c]);
+          }
+          if constexpr (b == 0 && !RES) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) out[c * OT + ot] = zero4();
+          }
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            out[c * OT + ot] = nx6_mma(a[0], a[1], a[2], xs[c], out[c * OT + ot]);
+          if constexpr (ACT && b == NB - 1) {
+            const f32x4 gg = gs[ot % NGS], J = out[ot], L = out[OT + ot];
+            out[ot] = gg * J;                                                // :686
+            out[OT + ot] = (10.f * gg * (1.f - gg)) * J * J + gg * L;        // :682-684
+          }
+        });
+  }
+  return;
+#endif
   f32x4 acc[G][2], gs[G];
   nbf16x8 xs[2][3];
   run_steps<STEPS, 3, 0, SITE_TAYLOR>(

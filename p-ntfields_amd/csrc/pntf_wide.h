@@ -46,7 +46,8 @@ __device__ __forceinline__ f32x16 zero16() {
 // scheme, pntf_gemm.hip x6_split: 2.67x the fp32 MFMA rate).  A 32-feature tile's registers
 // 8b..8b+7 are the B operand of k block b as they are (lane (j, h) holds feature rows
 // wrow(8b + i, h), i = 0..7); the weights are pre-split in the same k order (OFF_X6,
-// pack_x6_kernel).  encoder[0] and the Fourier fold stay on fp32 MFMA.
+// pack_x6_kernel).  encoder[0] runs split-bf16 as well (PNTF_X6_E0, default 1); only the
+// Fourier fold (encoder[0]^T fused with the Fourier Jacobian) stays on fp32 MFMA.
 #ifndef PNTF_WIDE_X6
 #define PNTF_WIDE_X6 0
 #endif
@@ -65,6 +66,11 @@ __device__ __forceinline__ void wx6_split(const f32x16& v, int b, wbf16x8 (&s)[3
     // whole split input bank live, 192 registers)
     if constexpr (OPAQUE) asm volatile("" : "+v"(x));
     const wbf16x2 p0 = __builtin_convertvector(x, wbf16x2);
+#ifdef PNTF_ABL_NOSPLIT   // diagnostics only (tests/diag ablations): one term, wrong results
+    s[0][2 * i] = s[1][2 * i] = s[2][2 * i] = p0[0];
+    s[0][2 * i + 1] = s[1][2 * i + 1] = s[2][2 * i + 1] = p0[1];
+    continue;
+#endif
     const wf32x2 r1 = x - __builtin_convertvector(p0, wf32x2);
     const wbf16x2 p1 = __builtin_convertvector(r1, wbf16x2);
     const wf32x2 r2 = r1 - __builtin_convertvector(p1, wf32x2);
@@ -75,11 +81,16 @@ __device__ __forceinline__ void wx6_split(const f32x16& v, int b, wbf16x8 (&s)[3
   }
 }
 // out tiles per group of an x6 layer: G accumulators of NC tiles live
+// PNTF_X6_ACC = 1 (round 6): the out bank is the accumulator and every layer's out tiles form
+// one group (xlayer below); the split copy is then in (kt, ot) step order for every layer
+#ifndef PNTF_X6_ACC
+#define PNTF_X6_ACC 0
+#endif
 #ifndef PNTF_X6_G1
-#define PNTF_X6_G1 4
+#define PNTF_X6_G1 (PNTF_X6_ACC ? 8 : 4)
 #endif
 #ifndef PNTF_X6_G2
-#define PNTF_X6_G2 1
+#define PNTF_X6_G2 (PNTF_X6_ACC ? 4 : 1)
 #endif
 #ifndef PNTF_X6_G1BUF
 #define PNTF_X6_G1BUF 1
@@ -113,6 +124,9 @@ __device__ __forceinline__ f32x16 wx6_mma(const f32x4& w0, const f32x4& w1, cons
 constexpr float WKAPPA = WIDE_KAPPA;                  // 10 / ln 2
 constexpr float WKAPPA_INV = 0.0693147180559945309f;  // ln 2 / 10
 __device__ __forceinline__ SpSig wsp_sig(float y) {   // y = κ·(pre-activation)
+#ifdef PNTF_ABL_CHEAPACT   // diagnostics only (tests/diag ablations): no transcendentals
+  return SpSig{fmaxf(y, 0.f) * 0.5f + 0.01f, 0.5f};
+#endif
   const float t = __builtin_amdgcn_exp2f(-fabsf(y));
   const float u = 1.f + t;
   const float r = __builtin_amdgcn_rcpf(u);
@@ -243,7 +257,7 @@ struct WHeadT {
   }
 };
 typedef WHeadT<false> WHead;
-typedef WHeadT<PNTF_WIDE_X6 && PNTF_X6_BM> WHeadE;   // an encoder layer (two columns)
+typedef WHeadT<PNTF_WIDE_X6 && PNTF_X6_BM && !PNTF_X6_ACC> WHeadE;   // an encoder layer (two columns)
 // fragments per step of whatever a step sequence hands over to (a WHead is always a wlayer)
 struct WE0Head;
 struct WFoldHead;
@@ -257,10 +271,13 @@ constexpr int wnext_nl();
 #endif
 constexpr bool WE0X6 = PNTF_WIDE_X6 && PNTF_X6_E0;
 constexpr int WE0NL = WE0X6 ? 6 : 4;   // fragments per encoder[0] step
-static_assert(!WE0X6 || PNTF_X6_G2 == 1, "encoder[0]'s split copy in per-tile order");
+static_assert(!WE0X6 || PNTF_X6_G2 == 1 || PNTF_X6_G2 == 4,
+              "encoder[0]'s split copy in per-tile (G2 = 1) or step (G2 = 4) order");
 struct WE0Head {
   __device__ int operator()(int j, int l) const {
-    if constexpr (WE0X6)
+    if constexpr (WE0X6 && PNTF_X6_G2 == 4)   // (kt, ot) order: the step order itself
+      return OFF_X6 * 4 + (WF + OFF_E0 * 4 - OFF_WIDE * 4) / 2 * 3 + (j * 6 + l) * 1024;
+    else if constexpr (WE0X6)
       return OFF_X6 * 4 + (WF + OFF_E0 * 4 - OFF_WIDE * 4) / 2 * 3 +
              ((((j % 4) * 8 + j / 4) * 6 + l) * 1024);
     else
@@ -288,8 +305,21 @@ struct WFoldHead {
       return WB + OFF_E0 * 4 + ((((o + 4 * half) * 4 + kt) * 4 + l) * 1024);
   }
 };
+// Fourier fold on split-bf16 in the accumulate engine (PNTF_X6_ACC, PNTF_XFOLD): step
+// S = (p·4 + kt)·4 + ot_local over two passes p of 4 out tiles (sin/cos rows of feature tiles
+// 2p, 2p + 1); the split copy of encoder[0]^T is packed in this order (pack_x6_kernel)
+#ifndef PNTF_XFOLD
+#define PNTF_XFOLD 1
+#endif
+constexpr bool XFOLD = PNTF_WIDE_X6 && PNTF_X6_ACC && PNTF_XFOLD;
+struct WFoldXHead {
+  __device__ int operator()(int j, int l) const {
+    return OFF_X6 * 4 + (WB + OFF_E0 * 4 - OFF_WIDE * 4) / 2 * 3 + (j * 6 + l) * 1024;
+  }
+};
 template <class F>
 constexpr int wnext_nl() {
+  if constexpr (std::is_same<F, WFoldXHead>::value) return 6;
   if constexpr (std::is_same<F, WE0Head>::value) return WE0NL;
   else if constexpr (std::is_same<F, WFoldHead>::value) return WFNL;
   else return std::is_same<F, WHead>::value || std::is_same<F, WHeadE>::value ? WNL : 4;
@@ -733,6 +763,77 @@ __device__ __forceinline__ float wide_forward(Ring& ring, Rsrc W, const PairIO& 
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-0.144269504088896341f * y4));
 }
 
+// ---- encoder[0]^T (256 x 128: OT 8, KT 4) fused with the Fourier Jacobian (:639-645), the
+// last phase of the reverse sweep; Y holds dL/d(encoder[0] output) (2 points x 4 tiles).
+template <int DIM, class BT, class AfterF>
+__device__ __forceinline__ void wide_fold(Ring& ring, Rsrc W, const PairIO& io, BT bt,
+                                          const f32x16 (&Y)[8], int lane, float (&ds)[DIM],
+                                          float (&dg)[DIM], AfterF after) {
+  const int h = lane >> 5;
+  // Feature tile o pairs sin rows (out tile o) with cos rows (out tile o + 4) of the same q;
+  // step (o, kt, half) accumulates half's out tile; after (o, 3, 1) the tile pair folds
+  //   dτ/dx_c += Σ_rows 2πB[:, f] (dφ_sin cos q_f - dφ_cos sin q_f)
+  float acc[2][DIM];
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) acc[0][d] = acc[1][d] = 0.f;
+  f32x16 ph[2][2];   // [sin | cos rows][point]
+  run_steps<32, WFNL, wnext_nl<AfterF>(), SITE_FOLD>(
+      ring, W, lane * 16, WFoldHead{}, after, [&](auto st, const f32x4 (&a)[WFNL]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int o = S / 8, kt = (S / 2) % 4, half = S % 2;
+        if constexpr (kt == 0) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) ph[half][c] = zero16();
+        }
+        if constexpr (WFX6) {
+          // (split per step: keeping it for the second half spills)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              wbf16x8 xs[3];
+              wx6_split<true>(Y[c * 4 + kt], b, xs);
+              ph[half][c] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs, ph[half][c]);
+            }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+              for (int c = 0; c < 2; ++c)
+                ph[half][c] = mfma32(a[u][s], Y[c * 4 + kt][4 * u + s], ph[half][c]);
+        }
+        if constexpr (kt == 3 && half == 1) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            f32x4 bw[DIM];
+#pragma unroll
+            for (int d = 0; d < DIM; ++d) bw[d] = TWO_PI * bt.load(io, d * H + 32 * o + 8 * u + 4 * h);
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int s = 0; s < 4; ++s) {
+                float q = 0.f;
+#pragma unroll
+                for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], bw[d][s], q);
+                float sn, cs;
+                sincos_fast(q, sn, cs);
+                const int r = 4 * u + s;
+                float gg = ph[0][c][r] * cs - ph[1][c][r] * sn;
+#pragma unroll
+                for (int d = 0; d < DIM; ++d) acc[c][d] = fmaf(bw[d][s], gg, acc[c][d]);
+              }
+          }
+        }
+      });
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) {
+    ds[d] = acc[0][d] + __shfl_xor(acc[0][d], 32);
+    dg[d] = acc[1][d] + __shfl_xor(acc[1][d], 32);
+  }
+}
+
 // ---------------------------------------------------------------- reverse sweep
 // Exact reverse mode (or out_backgrad when the forward stored the quirk).  On entry the ring
 // holds wbwd_head(); on return the first PF steps of `after`.  ds/dg: dτ/dxs, dτ/dxg of the
@@ -877,6 +978,618 @@ __device__ __forceinline__ void wide_backward(Ring& ring, Rsrc W, const PairIO& 
   }
 }
 
+#if PNTF_WIDE_X6 && PNTF_X6_ACC
+// ================================================================ accumulate-in-bank layers
+// Round 6.  The round-5 x6 layers issued their VALU in bursts the MFMAs
+// could not shadow: each group's input split right before the MFMAs that read it, and each out
+// tile's whole softplus/σ epilogue in one step (gfx950: a v_mfma_f32_32x32x16_bf16 leaves 24 of
+// its 32 cycles to independent VALU of the same wave, MI355X_MICROARCH.md; a step whose VALU
+// exceeds that serialises).  Here:
+//   * the out bank is the accumulator: out tile ot of the layer IS the MFMA C/D (the residual
+//     is its initial value, the bias one fp32 MFMA at kt = 0), so no accumulator registers are
+//     needed beside the two banks and every layer's out tiles form ONE group — each input tile
+//     is split once per layer (round 5: twice in the generator, 2-4 times in the encoder);
+//   * steps (kt, ot), ot fastest; the split of input tile kt + 1 (one-column layers) runs
+//     inside the OT steps of tile kt, one k block at a time, into the other half of a double
+//     buffer;
+//   * the epilogue runs in CHUNKS (4 registers of one out tile and column: the softplus/σ of 4
+//     elements and their 16-byte σ store, or the reverse sweep's σ multiply with its 16-byte
+//     σ load issued PDS steps ahead), CPS chunks per step from the step after the first out
+//     tile is final; the chunks that do not fit in the layer's last steps run in the first
+//     steps of the NEXT layer (its pre hook, XPend), each before that layer splits the tile.
+// Chunk j (tile t = j / (4 NC), column c = (j / 4) % NC, part q = j % 4) runs at step
+// E(j) = STEPS - OT + 1 + j / CPS of the layer (>= STEPS: the next layer's step E - STEPS).
+template <class L>
+struct XSched {
+  static constexpr int STEPS = L::OT * L::KT;
+  static constexpr int E(int j) { return STEPS - L::OT + 1 + j / L::CPS; }
+  static constexpr int P(int j) { return E(j) - L::PDS; }   // its σ prefetch (reverse)
+};
+// the chunks (and prefetches) of layer ly due at its step S (S >= STEPS: in the next layer)
+template <class L, int S>
+__device__ __forceinline__ void xdue(L& ly) {
+  if constexpr (L::NCH > 0) {
+    static_for<0, L::NCH>([&](auto jj) {
+      constexpr int j = decltype(jj)::value;
+      if constexpr (L::PF && XSched<L>::P(j) == S) ly.prefetch(j);
+    });
+    static_for<0, L::NCH>([&](auto jj) {
+      constexpr int j = decltype(jj)::value;
+      if constexpr (XSched<L>::E(j) == S) ly.chunk(j);
+    });
+  }
+}
+// the previous layer's pending chunks as the next layer's pre hook
+// diagnostics (PNTF_XNOPEND bit 0: forward layers, bit 1: reverse layers): no chunk crosses into
+// the next layer (xlayer flushes its pending chunks at its end)
+#ifndef PNTF_XNOPEND
+#define PNTF_XNOPEND 0
+#endif
+template <class L>
+struct XPend {
+  L& ly;
+  template <class ST>
+  __device__ __forceinline__ void operator()(ST) const {
+    if constexpr (!(PNTF_XNOPEND & (L::PF ? 2 : 1))) xdue<L, XSched<L>::STEPS + ST::value>(ly);
+  }
+};
+// ... or all at once (before a phase that reads the whole bank)
+template <class L>
+__device__ __forceinline__ void xflush(L& ly) {
+  if constexpr (L::NCH > 0) {
+    static_for<0, L::NCH>([&](auto jj) {
+      constexpr int j = decltype(jj)::value;
+      if constexpr (L::PF && XSched<L>::P(j) >= XSched<L>::STEPS) ly.prefetch(j);
+    });
+    static_for<0, L::NCH>([&](auto jj) {
+      constexpr int j = decltype(jj)::value;
+      if constexpr (XSched<L>::E(j) >= XSched<L>::STEPS) ly.chunk(j);
+    });
+  }
+}
+
+// split double buffer of one-column layers, and where in the OT steps of input tile kt the
+// two k blocks of tile kt + 1 are split
+#ifndef PNTF_X6_PIPE
+#define PNTF_X6_PIPE 0
+#endif
+// encoder[0]: its input tile split once per kt and shared by the 4 out tiles (0: per step)
+#ifndef PNTF_XE0SHARE
+#define PNTF_XE0SHARE 1
+#endif
+// Banks in the AGPR file: each accumulated out tile passes an empty asm with an AGPR operand
+// (the VGPR file then holds the ring, the splits and the epilogue's temporaries; the chunks
+// and splits read a bank through v_accvgpr_read).  Both banks VALU-written in the VGPR file,
+// as the compiler otherwise chooses, leaves no VGPRs for the rest (spills).
+#ifndef PNTF_XAGPR
+#define PNTF_XAGPR 2
+#endif
+__device__ __forceinline__ void xagpr(f32x16& t) {
+#if PNTF_XAGPR
+  asm("" : "+a"(t));
+#endif
+}
+// Each input tile is split once per layer here, so nothing invites the compiler to keep a
+// split bank live; the opaque copy of wx6_split (round 5) only costs moves (PNTF_XOPQ = 1 keeps it)
+#ifndef PNTF_XOPQ
+#define PNTF_XOPQ 0
+#endif
+constexpr bool XOPQ = PNTF_XOPQ;
+// sched_group_barrier interleave per step: (1 MFMA, XIGLP VALU) x MFMAs (0: off)
+#ifndef PNTF_XIGLP
+#define PNTF_XIGLP 0
+#endif
+
+// One Linear layer on split-bf16 MFMA, accumulating in ly.out (bank index c·OT + ot), input
+// bank `in` (c·KT + kt).  ly.init(ot) starts out tile ot at kt = 0 (bias MFMA / residual /
+// zero); ly's chunks run as above; pre(st) runs first in every step (the previous layer's
+// pending chunks, loads for the next layer).
+template <int OT, int KT, int NC, int SITE, class L, class PreF, class NextF>
+__device__ __forceinline__ void xlayer(Ring& ring, Rsrc W, int wbase, f32x16 (&in)[8],
+                                       int lane, L& ly, PreF pre, NextF naddr) {
+  static_assert(NC * KT <= 8 && NC * OT <= 8, "bank size");
+  static_assert(L::OT == OT && L::KT == KT && L::NC == NC, "layer object shape");
+  constexpr int STEPS = OT * KT;
+  constexpr bool PIPE = NC == 1 && PNTF_X6_PIPE;
+  constexpr int SB0 = OT / 4, SB1 = (3 * OT) / 4;   // split steps of blocks 0 / 1 of tile kt+1
+  wbf16x8 xs[PIPE ? 2 : 1][NC][2][3];
+  run_steps<STEPS, 6, wnext_nl<NextF>(), SITE>(
+      ring, W, lane * 16, WHead{wbase}, naddr, [&](auto st, const f32x4 (&a)[6]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int kt = S / OT, ot = S % OT, p = PIPE ? (kt & 1) : 0;
+        pre(st);
+        if constexpr (ot == 0 && (kt == 0 || !PIPE)) {
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) wx6_split<XOPQ>(in[c * KT + kt], b, xs[p][c][b]);
+        }
+        if constexpr (kt == 0) ly.init(ot);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+            ly.out[c * OT + ot] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs[p][c][b],
+                                          ly.out[c * OT + ot]);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) xagpr(ly.out[c * OT + ot]);
+#if PNTF_XAGPR == 2
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          xagpr(in[t]);
+          xagpr(ly.out[t]);
+        }
+#endif
+        if constexpr (PIPE && kt + 1 < KT) {
+          if constexpr (ot == SB0) wx6_split<XOPQ>(in[kt + 1], 0, xs[p ^ 1][0][0]);
+          if constexpr (ot == SB1) wx6_split<XOPQ>(in[kt + 1], 1, xs[p ^ 1][0][1]);
+        }
+        xdue<L, S>(ly);
+#if PNTF_XIGLP > 0
+        static_for<0, 12 * NC>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, PNTF_XIGLP, 0);
+        });
+#endif
+      });
+  if constexpr ((PNTF_XNOPEND & (L::PF ? 2 : 1)) != 0) xflush(ly);
+}
+
+// ---- layer objects: OT, KT, NC; CPS chunks per step; NCH chunks; PF/PDS: σ prefetch
+// forward Linear + softplus10: out = sp(A·in + b (+ out if RES)); σ10 saved when SAVE (scratch
+// tile sc0 + c·OT + t, or LDS tiles when IN_LDS); ACT0: encoder[0]'s compat quirk (:435-438)
+template <int OT_, int KT_, int NC_, bool RES, bool SAVE, bool IN_LDS = false, bool ACT0 = false>
+struct XFwdAct {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, CPS = NC_, NCH = NC_ * OT_ * 4, PDS = 0;
+  static constexpr bool PF = false;
+  f32x16 (&out)[8];
+  WScratch sc;
+  int sc0, lane;
+  BiasCols<OT_> bc;
+  WLds wl;
+  float cm;   // ACT0: 1 in compat mode
+  __device__ __forceinline__ void init(int ot) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      out[c * OT + ot] = mfma32(bc(ot), 1.f, RES ? out[c * OT + ot] : zero16());
+  }
+  __device__ __forceinline__ void prefetch(int) {}
+  __device__ __forceinline__ void chunk(int j) {
+    const int t = j / (4 * NC), c = (j / 4) % NC, q = j % 4;
+    f32x4 g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const SpSig v = wsp_sig(out[c * OT + t][4 * q + s]);
+      out[c * OT + t][4 * q + s] = v.sp;
+      g[s] = ACT0 ? fmaf(cm, __builtin_amdgcn_rcpf(2.f - v.sg) - v.sg, v.sg) : v.sg;
+    }
+    if constexpr (SAVE && IN_LDS) wl.p[((sc0 + c * OT + t) * 4 + q) * 64] = g;
+    else if constexpr (SAVE) bstore<PNTF_WSTORE_AUX>(sc.r, g, lane * 16, (sc0 + c * OT + t) * 4096 + q * 1024);
+  }
+};
+// forward Linear without activation (encoder[-1], :234): nothing pending
+template <int OT_, int KT_, int NC_>
+struct XFwdLin {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, CPS = 1, NCH = 0, PDS = 0;
+  static constexpr bool PF = false;
+  f32x16 (&out)[8];
+  BiasCols<OT_> bc;
+  __device__ __forceinline__ void init(int ot) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) out[c * OT + ot] = mfma32(bc(ot), 1.f, zero16());
+  }
+  __device__ __forceinline__ void prefetch(int) {}
+  __device__ __forceinline__ void chunk(int) {}
+};
+// reverse: out = (A^T·in (+ out if RES)) ⊙ σ tile mul0 + c·OT + t (if MUL); each chunk's σ part
+// is loaded PDS steps ahead into a ring of NSLOT registers quads
+#ifndef PNTF_XPDS
+#define PNTF_XPDS 3
+#endif
+template <int OT_, int KT_, int NC_, bool RES, bool MUL>
+struct XBwd {
+  static constexpr int OT = OT_, KT = KT_, NC = NC_, CPS = NC_, NCH = MUL ? NC_ * OT_ * 4 : 0;
+  static constexpr int PDS = PNTF_XPDS, NSLOT = CPS * (PDS + 1);
+  static constexpr bool PF = MUL;
+  f32x16 (&out)[8];
+  WScratch sc;
+  int mul0, lane;
+  f32x4 sg[NSLOT];
+  __device__ __forceinline__ void init(int ot) {
+    if constexpr (!RES) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) out[c * OT + ot] = zero16();
+    }
+  }
+  __device__ __forceinline__ void prefetch(int j) {
+    const int t = j / (4 * NC), c = (j / 4) % NC, q = j % 4;
+    sg[j % NSLOT] = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(sc.r, lane * 16,
+                                                     (mul0 + c * OT + t) * 4096 + q * 1024,
+                                                     AUX_LOAD));
+  }
+  __device__ __forceinline__ void chunk(int j) {
+    const int t = j / (4 * NC), c = (j / 4) % NC, q = j % 4;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) out[c * OT + t][4 * q + s] *= sg[j % NSLOT][s];
+  }
+};
+
+// ---------------------------------------------------------------- Fourier fold (x6 acc)
+// encoder[0]^T on split-bf16 MFMA fused with the Fourier Jacobian (:639-645).  Two passes; in
+// pass p the four out tiles sin(o), cos(o) for o = 2p, 2p + 1 accumulate in X (dead here:
+// X[c·4 + ot_local]) over the 4 input tiles of Y, each input tile split once per pass and
+// shared by the 4 tiles; after the pass the two feature tiles fold into dτ/dx_c as wide_fold.
+template <int DIM, class BT, class AfterF>
+__device__ __forceinline__ void wide_fold_x(Ring& ring, Rsrc W, const PairIO& io, BT bt,
+                                            f32x16 (&X)[8], f32x16 (&Y)[8], int lane,
+                                            float (&ds)[DIM], float (&dg)[DIM], AfterF after) {
+  const int h = lane >> 5;
+  float acc[2][DIM];
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) acc[0][d] = acc[1][d] = 0.f;
+  wbf16x8 xs[2][2][3];
+  run_steps<32, 6, wnext_nl<AfterF>(), SITE_FOLD>(
+      ring, W, lane * 16, WFoldXHead{}, after, [&](auto st, const f32x4 (&a)[6]) {
+        constexpr int S = decltype(st)::value;
+        constexpr int p = S / 16, kt = (S / 4) % 4, otl = S % 4;
+        if constexpr (otl == 0) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) wx6_split<XOPQ>(Y[c * 4 + kt], b, xs[c][b]);
+        }
+        if constexpr (kt == 0) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) X[c * 4 + otl] = zero16();
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            X[c * 4 + otl] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs[c][b], X[c * 4 + otl]);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) xagpr(X[c * 4 + otl]);
+#if PNTF_XAGPR == 2
+#pragma unroll
+        for (int t = 0; t < 8; ++t) xagpr(Y[t]);   // both banks in the AGPR file (as xlayer)
+#endif
+        // after the pass: feature tiles o = 2p + ol, sin rows X[c·4 + 2 ol], cos X[c·4 + 2 ol + 1]
+        if constexpr (kt == 3 && otl == 3) {
+#pragma unroll
+          for (int ol = 0; ol < 2; ++ol) {
+            const int o = 2 * p + ol;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              f32x4 bw[DIM];
+#pragma unroll
+              for (int d = 0; d < DIM; ++d)
+                bw[d] = TWO_PI * bt.load(io, d * H + 32 * o + 8 * u + 4 * h);
+#pragma unroll
+              for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                  float q = 0.f;
+#pragma unroll
+                  for (int d = 0; d < DIM; ++d) q = fmaf(io.x[c][d], bw[d][s], q);
+                  float sn, cs;
+                  sincos_fast(q, sn, cs);
+                  const int r = 4 * u + s;
+                  const float gg = X[c * 4 + 2 * ol][r] * cs - X[c * 4 + 2 * ol + 1][r] * sn;
+#pragma unroll
+                  for (int d = 0; d < DIM; ++d) acc[c][d] = fmaf(bw[d][s], gg, acc[c][d]);
+                }
+            }
+          }
+        }
+      });
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) {
+    ds[d] = acc[0][d] + __shfl_xor(acc[0][d], 32);
+    dg[d] = acc[1][d] + __shfl_xor(acc[1][d], 32);
+  }
+}
+
+// ---------------------------------------------------------------- forward pass (x6 acc)
+// As wide_forward; the encoder[0] epilogue and every layer's run as chunks (above).
+template <int DIM, bool GRAD, class BT, class AfterF>
+__device__ __forceinline__ float wide_forward_x(Ring& ring, Rsrc W, const PairIO& io, BT bt,
+                                                f32x16 (&X)[8], f32x16 (&Y)[8], WScratch sc,
+                                                WLds wl, int compat, int lane, AfterF after) {
+  const int h = lane >> 5;
+  // ---- encoder[0] (:186-190, :227), k-tile outer: X[c·4 + ot] accumulate 4 out tiles x 2
+  // points; sin tiles (kt < 4) are computed at step (kt, 0), their cos partners (kt + 4)
+  // kept in Y[c·4 + kt] until then; the input tile (sin or cos) is split once per kt and
+  // shared by the 4 out tiles
+  XFwdAct<4, 8, 2, false, GRAD, false, true> e0{X, sc, WT_E0, lane, {}, wl, compat ? 1.f : 0.f};
+  e0.bc.load(W, lane, B_E0);
+  XFwdAct<4, 4, 2, false, GRAD> a0{Y, sc, WT_EBLK, lane, {}, wl, 0.f};
+  {
+    f32x16 q[2], sn[2];
+    wbf16x8 xs[2][2][3];
+    wfourier_q<DIM>(io, bt, 0, h, q);
+    run_steps<32, WE0NL, WNL, SITE_FWD_E0>(
+        ring, W, lane * 16, WE0Head{}, WHead{WF + OFF_EBLK * 4},
+        [&](auto st, const f32x4 (&a)[WE0NL]) {
+          constexpr int S = decltype(st)::value;
+          constexpr int kt = S / 4, ot = S % 4;
+          if constexpr (ot == 0 && kt < 4) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                float x0, x1;
+                sincos_fast(q[c][r], x0, x1);
+                sn[c][r] = x0;
+                Y[c * 4 + kt][r] = x1;
+              }
+          }
+          if constexpr (ot == 0 || !PNTF_XE0SHARE) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int b = 0; b < 2; ++b)
+                wx6_split<XOPQ>(kt < 4 ? sn[c] : Y[c * 4 + (kt & 3)], b, xs[c][b]);
+          }
+          if constexpr (kt == 0) e0.init(ot);
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+              X[c * 4 + ot] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs[c][b], X[c * 4 + ot]);
+#pragma unroll
+          for (int c = 0; c < 2; ++c) xagpr(X[c * 4 + ot]);
+#if PNTF_XAGPR == 2
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            xagpr(X[t]);
+            if (kt >= 4 || t % 4 < kt) xagpr(Y[t]);   // the cos tiles already computed
+          }
+#endif
+          // next sin/cos tile's projections, after this tile's MFMAs are issued
+          if constexpr (ot == 3 && kt < 3) wfourier_q<DIM>(io, bt, kt + 1, h, q);
+          if constexpr (S == 16) a0.bc.load(W, lane, B_EBLK);
+          xdue<decltype(e0), S>(e0);
+        });
+  }
+
+  // ---- encoder residual blocks (:228-232); X = h (2 points x 4 tiles).  Each layer's bias
+  // columns are fetched at the first step of the layer before it.
+  const int WE = WF + OFF_EBLK * 4;
+  {
+    XFwdAct<4, 4, 2, true, GRAD> b0{X, sc, WT_EBLK + 8, lane, {}, wl, 0.f};
+    XFwdAct<4, 4, 2, false, GRAD> a1{Y, sc, WT_EBLK + 16, lane, {}, wl, 0.f};
+    XFwdAct<4, 4, 2, true, GRAD> b1{X, sc, WT_EBLK + 24, lane, {}, wl, 0.f};
+    XFwdLin<4, 4, 2> e3{Y, {}};
+    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WE, X, lane, a0,
+                                  both(XPend<decltype(e0)>{e0},
+                                       at<0>([&] { b0.bc.load(W, lane, B_EBLK + 128); })),
+                                  WHead{WE + SZ_E * 4});
+    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WE + SZ_E * 4, Y, lane, b0,
+                                  both(XPend<decltype(a0)>{a0},
+                                       at<0>([&] { a1.bc.load(W, lane, B_EBLK + 256); })),
+                                  WHead{WE + 2 * SZ_E * 4});
+    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
+                                  both(XPend<decltype(b0)>{b0},
+                                       at<0>([&] { b1.bc.load(W, lane, B_EBLK + 384); })),
+                                  WHead{WE + 3 * SZ_E * 4});
+    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
+                                  both(XPend<decltype(a1)>{a1},
+                                       at<0>([&] { e3.bc.load(W, lane, B_E3); })),
+                                  WHead{WF + OFF_E3 * 4});
+    // ---- encoder[-1] (:234) -> Y (zs = Y[0..3], zg = Y[4..7])
+    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WF + OFF_E3 * 4, X, lane, e3, XPend<decltype(b1)>{b1},
+                                  WHead{WF + OFF_GBLK * 4});
+  }
+
+  // ---- symmetric smooth max / min merge (:236-244) -> X (u = [M | m], 8 tiles)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 s0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float zs = Y[t][r], zg = Y[4 + t][r];   // κ-scaled
+      float d = zs - zg;
+      float e = __builtin_amdgcn_exp2f(-fabsf(d));    // e^{-10|zs - zg|}
+      float cc = __builtin_amdgcn_logf(1.f + e);      // κ·0.1·ln(1 + e)
+      X[t][r] = fmaxf(zs, zg) + cc;
+      X[4 + t][r] = fminf(zs, zg) - cc;
+      float rr = __builtin_amdgcn_rcpf(1.f + e);
+      s0[r] = (d >= 0.f) ? rr : e * rr;
+    }
+    if (GRAD) lstore(wl, WL_S0 + t, s0);
+  }
+
+  // ---- generator residual blocks (:246-249), rotated so that one loop body carries a
+  // layer's pending chunks into the next: ga0; (gb_i, ga_{i+1}) for i = 0, 1; gb2; g3
+  XFwdAct<8, 8, 1, false, GRAD> ga{Y, sc, WT_GBLK, lane, {}, wl, 0.f};
+  XFwdAct<8, 8, 1, true, GRAD> gb{X, sc, WT_GBLK + 8, lane, {}, wl, 0.f};
+  ga.bc.load(W, lane, B_GBLK);
+  xlayer<8, 8, 1, SITE_FWD_GEN>(ring, W, WF + OFF_GBLK * 4, X, lane, ga,
+                                at<0>([&] { gb.bc.load(W, lane, B_GBLK + 256); }),
+                                WHead{WF + (OFF_GBLK + SZ_G) * 4});
+#pragma unroll 1
+  for (int i = 0; i < 2; ++i) {
+    const int wb = opaque(WF + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4);
+    const int wa = opaque(WF + (OFF_GBLK + (2 * i + 2) * SZ_G) * 4);
+    const int wn = opaque(WF + (OFF_GBLK + (2 * i + 3) * SZ_G) * 4);
+    const int ba = opaque(B_GBLK + (2 * i + 2) * 256);
+    gb.sc0 = opaque(WT_GBLK + 16 * i + 8);
+    xlayer<8, 8, 1, SITE_FWD_GEN>(ring, W, wb, Y, lane, gb,
+                                  both(XPend<decltype(ga)>{ga},
+                                       at<0>([&] { ga.bc.load(W, lane, ba); })),
+                                  WHead{wa});
+    ga.sc0 = opaque(WT_GBLK + 16 * i + 16);
+    xlayer<8, 8, 1, SITE_FWD_GEN>(ring, W, wa, X, lane, ga,
+                                  both(XPend<decltype(gb)>{gb},
+                                       at<0>([&] { gb.bc.load(W, lane, ba + 256); })),
+                                  WHead{wn});
+  }
+  // ---- generator block 2's second layer, then generator[-2] + act (:251-252) -> Y[0..3]
+  XFwdAct<4, 8, 1, false, GRAD, true> g3{Y, sc, WL_G3, lane, {}, wl, 0.f};
+  gb.sc0 = WT_GBLK + 16 * 2 + 8;
+  xlayer<8, 8, 1, SITE_FWD_GEN>(ring, W, WF + (OFF_GBLK + 5 * SZ_G) * 4, Y, lane, gb,
+                                both(XPend<decltype(ga)>{ga},
+                                     at<0>([&] { g3.bc.load(W, lane, B_G3); })),
+                                WHead{WF + OFF_G3 * 4});
+  xlayer<4, 8, 1, SITE_FWD_GEN>(ring, W, WF + OFF_G3 * 4, X, lane, g3, XPend<decltype(gb)>{gb},
+                                after);
+  xflush(g3);
+  // ---- head generator[-1] + sigmoid(0.1 y) (:254-255)
+  float part = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      f32x4 w = whw_load(wl, t, u, h);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) part = fmaf(w[s], Y[t][4 * u + s], part);
+    }
+  part += __shfl_xor(part, 32);
+  const float y4 = fmaf(part, WKAPPA_INV, bload(W, 0, WG4B)[0]);   // part = κ·(g4w·h3)
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-0.144269504088896341f * y4));
+}
+
+// ---------------------------------------------------------------- reverse sweep (x6 acc)
+template <int DIM, class BT, class AfterF>
+__device__ __forceinline__ void wide_backward_x(Ring& ring, Rsrc W, const PairIO& io, BT bt,
+                                                float tau, f32x16 (&X)[8], f32x16 (&Y)[8],
+                                                WScratch sc, WLds wl, int lane,
+                                                float (&ds)[DIM], float (&dg)[DIM],
+                                                AfterF after) {
+  const int h = lane >> 5;
+  // ---- head and generator[-2] (:592-613): Y[t] = d · g4w ⊙ σ10(y3)
+  const float dd = 0.1f * tau * (1.f - tau);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 s3 = lload(wl, WL_G3 + t);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      f32x4 w = whw_load(wl, t, u, h);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) Y[t][4 * u + s] = (dd * w[s]) * s3[4 * u + s];
+    }
+  }
+#if defined(PNTF_XMIXB) && PNTF_XMIXB == 2   // diagnostics: the round-5 generator layers
+  // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> X   (G3^T: 256 x 128, OT 8, KT 4)
+  {
+    WBwd<8, 4, 1, false, true> l{X, sc, WT_GBLK + 16 * 2 + 8, lane};
+    wlayer<8, 4, 1, SITE_BWD_GEN, 4>(ring, W, WB + OFF_G3 * 4, Y, lane, l, NoPre{},
+                                     WHead{WB + (OFF_GBLK + 5 * SZ_G) * 4});
+  }
+  // ---- generator blocks, reverse (:615-618): blocks 2 and 1 in a loop, block 0 peeled (its
+  // second layer multiplies by no σ and hands over to encoder[-1]^T)
+#pragma unroll 1
+  for (int i = 2; i >= 1; --i) {
+    const int wa = opaque(WB + (OFF_GBLK + (2 * i) * SZ_G) * 4);
+    const int wb = opaque(WB + (OFF_GBLK + (2 * i + 1) * SZ_G) * 4);
+    const int wn = opaque(WB + (OFF_GBLK + (2 * i - 1) * SZ_G) * 4);
+    // da = (G1_i^T dr) ⊙ σ10(y1_i) -> Y
+    WBwd<8, 8, 1, false, true> lb{Y, sc, WT_GBLK + 16 * i, lane};
+    wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, wb, X, lane, lb, NoPre{}, WHead{wa});
+    // du = G_i^T da + dr, then ⊙ σ10(y2_{i-1})
+    WBwd<8, 8, 1, true, true> la{X, sc, WT_GBLK + 16 * (i - 1) + 8, lane};
+    wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, wa, Y, lane, la, NoPre{}, WHead{wn});
+  }
+  {
+    WBwd<8, 8, 1, false, true> lb{Y, sc, WT_GBLK, lane};
+    wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, WB + (OFF_GBLK + 1 * SZ_G) * 4, X, lane, lb,
+                                     NoPre{}, WHead{WB + OFF_GBLK * 4});
+    WBwd<8, 8, 1, true, false> la{X, sc, 0, lane};
+    wlayer<8, 8, 1, SITE_BWD_GEN, 4>(ring, W, WB + OFF_GBLK * 4, Y, lane, la, NoPre{},
+                                     WHeadE{WB + OFF_E3 * 4});
+  }
+#else
+  // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> X   (G3^T: 256 x 128, OT 8, KT 4)
+  XBwd<8, 4, 1, false, true> l3{X, sc, WT_GBLK + 16 * 2 + 8, lane, {}};
+  xlayer<8, 4, 1, SITE_BWD_GEN>(ring, W, WB + OFF_G3 * 4, Y, lane, l3, NoPre{},
+                                WHead{WB + (OFF_GBLK + 5 * SZ_G) * 4});
+  // ---- generator blocks, reverse (:615-618), rotated: lb_2; (la_i, lb_{i-1}) for i = 2, 1;
+  // la_0 (no σ: it hands over to encoder[-1]^T)
+  XBwd<8, 8, 1, false, true> lb{Y, sc, WT_GBLK + 16 * 2, lane, {}};
+  XBwd<8, 8, 1, true, true> la{X, sc, 0, lane, {}};
+  xlayer<8, 8, 1, SITE_BWD_GEN>(ring, W, WB + (OFF_GBLK + 5 * SZ_G) * 4, X, lane, lb,
+                                XPend<decltype(l3)>{l3}, WHead{WB + (OFF_GBLK + 4 * SZ_G) * 4});
+#pragma unroll 1
+  for (int i = 2; i >= 1; --i) {
+    const int wa = opaque(WB + (OFF_GBLK + (2 * i) * SZ_G) * 4);
+    const int wb = opaque(WB + (OFF_GBLK + (2 * i - 1) * SZ_G) * 4);
+    const int wn = opaque(WB + (OFF_GBLK + (2 * i - 2) * SZ_G) * 4);
+    // du = G_i^T da + dr, then ⊙ σ10(y2_{i-1})
+    la.mul0 = opaque(WT_GBLK + 16 * (i - 1) + 8);
+    xlayer<8, 8, 1, SITE_BWD_GEN>(ring, W, wa, Y, lane, la, XPend<decltype(lb)>{lb}, WHead{wb});
+    // da = (G1_{i-1}^T dr) ⊙ σ10(y1_{i-1}) -> Y
+    lb.mul0 = opaque(WT_GBLK + 16 * (i - 1));
+    xlayer<8, 8, 1, SITE_BWD_GEN>(ring, W, wb, X, lane, lb, XPend<decltype(la)>{la}, WHead{wn});
+  }
+  {
+    XBwd<8, 8, 1, true, false> l0{X, sc, 0, lane, {}};
+    xlayer<8, 8, 1, SITE_BWD_GEN>(ring, W, WB + OFF_GBLK * 4, Y, lane, l0,
+                                  XPend<decltype(lb)>{lb}, WHead{WB + OFF_E3 * 4});
+  }
+#endif
+  // ---- merge Jacobian (:620-627): X[0..3] = dzs, X[4..7] = dzg
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    f32x16 s0 = lload(wl, WL_S0 + t);
+    f32x16 s1 = 1.f - s0;
+    f32x16 dM = X[t], dm = X[4 + t];
+    X[t] = s0 * dM + s1 * dm;
+    X[4 + t] = s1 * dM + s0 * dm;
+  }
+#if defined(PNTF_XMIXB) && PNTF_XMIXB == 1   // diagnostics: the round-5 encoder layers
+  // ---- encoder[-1]^T ⊙ σ10(y2 of encoder block 1), then the blocks, reverse (:629-636)
+  const int WE = WB + OFF_EBLK * 4;
+  {
+    WBwd<4, 4, 2, false, true> e3{Y, sc, WT_EBLK + 24, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
+                                     WHeadE{WE + 3 * SZ_E * 4});
+    WBwd<4, 4, 2, false, true> b1{X, sc, WT_EBLK + 16, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, NoPre{},
+                                     WHeadE{WE + 2 * SZ_E * 4});
+    WBwd<4, 4, 2, true, true> a1{Y, sc, WT_EBLK + 8, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
+                                     WHeadE{WE + 1 * SZ_E * 4});
+    WBwd<4, 4, 2, false, true> b0{X, sc, WT_EBLK, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, NoPre{},
+                                     WHeadE{WE});
+    WBwd<4, 4, 2, true, true> a0{Y, sc, WT_E0, lane};
+    wlayer<4, 4, 2, SITE_BWD_ENC, 4>(ring, W, WE, X, lane, a0, NoPre{}, WFoldHead{});
+  }
+
+  wide_fold<DIM>(ring, W, io, bt, Y, lane, ds, dg, after);
+  return;
+#else
+  // ---- encoder[-1]^T ⊙ σ10(y2 of encoder block 1), then the blocks, reverse (:629-636)
+  const int WE = WB + OFF_EBLK * 4;
+  {
+    XBwd<4, 4, 2, false, true> e3{Y, sc, WT_EBLK + 24, lane, {}};
+    XBwd<4, 4, 2, false, true> b1{X, sc, WT_EBLK + 16, lane, {}};
+    XBwd<4, 4, 2, true, true> a1{Y, sc, WT_EBLK + 8, lane, {}};
+    XBwd<4, 4, 2, false, true> b0{X, sc, WT_EBLK, lane, {}};
+    XBwd<4, 4, 2, true, true> a0{Y, sc, WT_E0, lane, {}};
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
+                                  WHead{WE + 3 * SZ_E * 4});
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, XPend<decltype(e3)>{e3},
+                                  WHead{WE + 2 * SZ_E * 4});
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, XPend<decltype(b1)>{b1},
+                                  WHead{WE + 1 * SZ_E * 4});
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, XPend<decltype(a1)>{a1},
+                                  WHead{WE});
+    if constexpr (XFOLD)
+      xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE, X, lane, a0, XPend<decltype(b0)>{b0},
+                                    WFoldXHead{});
+    else
+      xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE, X, lane, a0, XPend<decltype(b0)>{b0},
+                                    WFoldHead{});
+    xflush(a0);
+  }
+#endif
+  if constexpr (XFOLD) wide_fold_x<DIM>(ring, W, io, bt, X, Y, lane, ds, dg, after);
+  else wide_fold<DIM>(ring, W, io, bt, Y, lane, ds, dg, after);
+}
+#endif  // PNTF_WIDE_X6 && PNTF_X6_ACC
+
 // ---------------------------------------------------------------- kernel
 template <int DIM, int KIND, bool BL>
 __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
@@ -923,15 +1636,30 @@ __global__ __launch_bounds__(256, 1) void wide_field_kernel(FieldArgs a) {
     WBt<BL> bt;
     if constexpr (BL) bt.t = (const wlds_f*)wbtab + (io.Bw - a.Btab);
     float tau;
+#if PNTF_WIDE_X6 && PNTF_X6_ACC && defined(PNTF_XMIX) && PNTF_XMIX == 1   // diagnostics
+#define PNTF_WFWD wide_forward_x
+#define PNTF_WBWD wide_backward
+#elif PNTF_WIDE_X6 && PNTF_X6_ACC && defined(PNTF_XMIX) && PNTF_XMIX == 2
+#define PNTF_WFWD wide_forward
+#define PNTF_WBWD wide_backward_x
+#elif PNTF_WIDE_X6 && PNTF_X6_ACC
+#define PNTF_WFWD wide_forward_x
+#define PNTF_WBWD wide_backward_x
+#else
+#define PNTF_WFWD wide_forward
+#define PNTF_WBWD wide_backward
+#endif
     if constexpr (GRAD)
-      tau = wide_forward<DIM, true>(ring, W, io, bt, X, Y, sc, wl, a.compat, lane, wbwd_head());
+      tau = PNTF_WFWD<DIM, true>(ring, W, io, bt, X, Y, sc, wl, a.compat, lane, wbwd_head());
     else
-      tau = wide_forward<DIM, false>(ring, W, io, bt, X, Y, sc, wl, a.compat, lane, WE0Head{});
+      tau = PNTF_WFWD<DIM, false>(ring, W, io, bt, X, Y, sc, wl, a.compat, lane, WE0Head{});
     float ds[DIM], dg[DIM];
     if constexpr (GRAD) {
       drain_stores();
-      wide_backward<DIM>(ring, W, io, bt, tau, X, Y, sc, wl, lane, ds, dg, WE0Head{});
+      PNTF_WBWD<DIM>(ring, W, io, bt, tau, X, Y, sc, wl, lane, ds, dg, WE0Head{});
     }
+#undef PNTF_WFWD
+#undef PNTF_WBWD
     const bool store = lane < 32 && pair < a.n;
     store_field<DIM, KIND>(a, pair, ok, store, tau, io, ds, dg);
   }
@@ -977,7 +1705,13 @@ __global__ void pack_x6_kernel(const float* __restrict__ wide, uint16_t* __restr
   const int j = (f - m0) / 1024, ot = j / KT, kt = j % KT;
   // first fragment of (ot, kt, block b) in the x6 step order of wlayer; term p at + p
   int64_t fr;
-  if (bm && nc == 2) {   // step (g, kt, b), fragments 3o + p
+  if (PNTF_X6_ACC && PNTF_XFOLD && !bm && dir && m0 == OFF_E0) {
+    // encoder[0]^T for the accumulate engine's fold: pass p = (ot % 4) / 2 covers feature tiles
+    // 2p, 2p + 1 with their sin (ot < 4) and cos (ot >= 4) rows; step (p, kt, ot_local),
+    // ot_local = ((ot % 4) % 2)·2 + ot / 4, fragments 3b + term
+    const int pp = (ot % 4) / 2, ol = ((ot % 4) % 2) * 2 + ot / 4;
+    fr = ((int64_t)(gf - j) + (pp * KT + kt) * 4 + ol) * 6 + 3 * b;
+  } else if (bm && nc == 2) {   // step (g, kt, b), fragments 3o + p
     fr = ((int64_t)(gf - j) + ((ot / 2) * KT + kt) * 2 + b) * 6 + (ot % 2) * 3;
   } else {                     // step (g, kt, o), fragments 3b + p
     const int G = wx6_group(OT, nc);

@@ -12,7 +12,8 @@ import torch
 
 from pntf import ops
 from pntf import train as _train
-from pntf.net import PackedCache, build_layers, guard_epilogue, out_tau, taylor_outputs
+from pntf.net import (PackedCache, build_layers, compose_speed, compose_travel_time,
+                      compose_velocity, out_tau, records_weights, taylor_outputs)
 from pntf.net import init_weights as _init_weights
 
 from .model_res_sigmoid_multi import (DDSigmoid_out, DSigmoid, DSigmoid_out, Sigmoid,  # noqa
@@ -276,22 +277,28 @@ class Model:
     def _dev(self):
         return torch.device(self.Params["Device"])
 
+    # fused kernels, or (autograd recording, trainable weights) composed from the
+    # differentiable NN.out / out_grad as the reference's torch graphs
     def TravelTimes(self, Xp):
         Xp = Xp.to(self._dev())
-        out = ops.travel_time(self.network.packed(), Xp, self.network._B(Xp.device), None,
-                              self.dim)
-        return guard_epilogue(self.network, out, "Model.TravelTimes")
+        if records_weights(self.network):
+            return compose_travel_time(self.network.out(Xp)[0], Xp, self.dim)
+        return ops.travel_time(self.network.packed(), Xp, self.network._B(Xp.device), None,
+                               self.dim)
 
     def Tau(self, Xp):
         Xp = Xp.to(self._dev())
-        out = ops.tau(self.network.packed(), Xp, self.network._B(Xp.device), None,
-                      self.dim).unsqueeze(1)
-        return guard_epilogue(self.network, out, "Model.Tau")
+        if records_weights(self.network):
+            return self.network.out(Xp)[0]
+        return ops.tau(self.network.packed(), Xp, self.network._B(Xp.device), None,
+                       self.dim).unsqueeze(1)
 
     def Speed(self, Xp):
         Xp = Xp.to(self._dev())
-        out = ops.speed(self.network.packed(), Xp, self.network._B(Xp.device), None, self.dim)
-        return guard_epilogue(self.network, out, "Model.Speed")
+        if records_weights(self.network):
+            tau, dtau, _ = self.network.out_grad(Xp)
+            return compose_speed(tau, dtau, Xp, self.dim)
+        return ops.speed(self.network.packed(), Xp, self.network._B(Xp.device), None, self.dim)
 
     def Speed2(self, Xp, gamma):
         """Speed at the goal with the viscosity term (:1218-1245): 1 / (sqrt(S)/τ² + γ Δ_gτ)
@@ -310,9 +317,12 @@ class Model:
     def Gradient(self, Xp):
         """Path velocity from the exact ∇τ (autograd in the reference, :1247-1282)."""
         Xp = Xp.to(self._dev())
+        if records_weights(self.network):
+            tau, dtau, _ = self.network.out_grad(Xp)
+            return compose_velocity(tau, dtau, Xp, self.dim)
         v, _ = ops.path_velocity(self.network.packed(), Xp, self.network._B(Xp.device), None,
                                  self.dim, ops.GRAD_EXACT)
-        return guard_epilogue(self.network, v, "Model.Gradient")
+        return v
 
     def Plan(self, XP, step=0.015, tol=0.03, max_iter=300):
         """Batched test/arm_plan.py:140-152 loop on device (exact ∇τ, per-query freeze)."""

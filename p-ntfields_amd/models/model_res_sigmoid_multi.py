@@ -29,7 +29,8 @@ import torch
 
 from pntf import ops
 from pntf import train as _train
-from pntf.net import PackedCache, build_layers, guard_epilogue, out_tau, taylor_outputs
+from pntf.net import (PackedCache, build_layers, compose_speed, compose_travel_time,
+                      compose_velocity, out_tau, records_weights, taylor_outputs)
 from pntf.net import init_weights as _init_weights
 
 
@@ -321,34 +322,44 @@ class Model:
     def _dev(self):
         return torch.device(self.Params["Device"])
 
+    # The epilogues run as fused kernels; when autograd records and the weights require grad
+    # they are composed from the differentiable NN.out / out_grad / out_backgrad instead, so a
+    # loss on them trains the weights as the reference's torch graphs do.
     def TravelTimes(self, Xp):
         """|x_g - x_s| / τ (:1173-1186), uses self.B."""
         Xp = Xp.to(self._dev())
-        out = ops.travel_time(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
-                              self.dim)
-        return guard_epilogue(self.network, out, "Model.TravelTimes")
+        if records_weights(self.network):
+            return compose_travel_time(self.network.out(Xp, self.B)[0], Xp, self.dim)
+        return ops.travel_time(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                               self.dim)
 
     def Tau(self, Xp):
         """τ (N,1) (:1188-1193), uses self.B."""
         Xp = Xp.to(self._dev())
-        out = ops.tau(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
-                      self.dim).unsqueeze(1)
-        return guard_epilogue(self.network, out, "Model.Tau")
+        if records_weights(self.network):
+            return self.network.out(Xp, self.B)[0]
+        return ops.tau(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                       self.dim).unsqueeze(1)
 
     def Speed(self, Xp):
         """Speed at the goal (:1195-1216), uses self.B."""
         Xp = Xp.to(self._dev())
-        out = ops.speed(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
-                        self.dim)
-        return guard_epilogue(self.network, out, "Model.Speed")
+        if records_weights(self.network):
+            tau, dtau, _ = self.network.out_grad(Xp, self.B)
+            return compose_speed(tau, dtau, Xp, self.dim)
+        return ops.speed(self.network.packed(), Xp, _as_table(self.B, Xp.device), None,
+                         self.dim)
 
     def Gradient(self, Xp, B, env=None):
         """Path velocity [v_s | v_g] (:1218-1248) from the out_backgrad sweep (quirk kept),
         per-row norms."""
         Xp = Xp.to(self._dev())
+        if records_weights(self.network):
+            tau, dtau, _ = self.network.out_backgrad(Xp, B, env)
+            return compose_velocity(tau, dtau, Xp, self.dim)
         v, _ = ops.path_velocity(self.network.packed(), Xp, _as_table(B, Xp.device), env,
                                  self.dim, ops.GRAD_BACKGRAD_COMPAT)
-        return guard_epilogue(self.network, v, "Model.Gradient")
+        return v
 
     def Plan(self, XP, B, step=0.03, tol=0.06, max_iter=500, env=None,
              mode=ops.GRAD_BACKGRAD_COMPAT):

@@ -281,30 +281,39 @@ def out_tau(module, coords, B, env, dim):
     return tau if wt is None else tau + wt
 
 
-class _EpilogueOutput(torch.autograd.Function):
-    """Marks the output of a fused epilogue kernel (Model.Speed / Tau / TravelTimes / Gradient)
-    as depending on the weights without a HIP gradient for it: a backward that reaches it
-    raises instead of silently leaving the weights untouched (the reference's versions are
-    torch graphs; a loss belongs on NN.out / out_grad / out_laplace, which differentiate)."""
-
-    @staticmethod
-    def forward(ctx, what, out, *params):
-        ctx.what = what
-        return out.view_as(out)
-
-    @staticmethod
-    def backward(ctx, *g):
-        raise ops.PntfError(
-            "%s comes from a fused HIP epilogue kernel with no gradient; write the loss on "
-            "NN.out / NN.out_grad / NN.out_laplace (differentiable) instead" % ctx.what)
+def records_weights(module):
+    """True when autograd records a graph and a parameter of `module` requires grad: the
+    drop-in Model epilogues (Speed / Tau / TravelTimes / Gradient) then compose their output
+    from the differentiable NN.out / out_grad / out_backgrad, as the reference's torch graphs
+    do (models/model_res_sigmoid_multi.py:1173-1248), instead of the fused epilogue kernels."""
+    return torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters())
 
 
-def guard_epilogue(module, out, what):
-    """`out` unchanged, or (autograd recording, trainable weights) wrapped so that
-    differentiating it raises (_EpilogueOutput)."""
-    if not torch.is_grad_enabled():
-        return out
-    ps = [p for p in module.parameters() if p.requires_grad]
-    if not ps:
-        return out
-    return _EpilogueOutput.apply(what, out, *ps)
+def compose_travel_time(tau, Xp, dim):
+    """Model.TravelTimes (:1173-1186): sqrt(|x_g - x_s|²) / τ."""
+    D = Xp[:, dim:] - Xp[:, :dim]
+    return torch.sqrt(torch.einsum("ij,ij->i", D, D)) / tau[:, 0]
+
+
+def compose_speed(tau, dtau, Xp, dim):
+    """Model.Speed (:1195-1216): τ² / sqrt(T0 |∇_g τ|² - 2 τ ∇_g τ·D + τ²)."""
+    D = Xp[:, dim:] - Xp[:, :dim]
+    T0 = torch.einsum("ij,ij->i", D, D)
+    DT1 = dtau[:, dim:]
+    T3 = tau[:, 0] ** 2
+    S = T0 * torch.einsum("ij,ij->i", DT1, DT1) - 2 * tau[:, 0] * torch.einsum("ij,ij->i", DT1, D) + T3
+    return T3 / torch.sqrt(S)
+
+
+def compose_velocity(tau, dtau, Xp, dim):
+    """Model.Gradient (:1218-1248): [v_start | v_goal], each row normalised by its own norm
+    (the arm reference's whole-tensor norm only defines a batch of one)."""
+    D = Xp[:, dim:] - Xp[:, :dim]
+    T0 = torch.sqrt(torch.einsum("ij,ij->i", D, D))
+    T3 = tau[:, 0] ** 2
+    out = []
+    for V0, V1 in ((-D, dtau[:, :dim]), (D, dtau[:, dim:])):
+        Y = -(1 / (T0 * tau[:, 0]).unsqueeze(1) * V0 - (T0 / T3).unsqueeze(1) * V1)
+        S = torch.norm(Y, p=2, dim=1).unsqueeze(1)
+        out.append(1 / S ** 2 * Y)
+    return torch.cat(out, dim=1)

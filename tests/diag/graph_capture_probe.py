@@ -14,9 +14,14 @@ modes (each in its own process; run the ones expected to crash last):
   profiler_then_abi   a torch.profiler CUDA-activity session first (as
                       tests/test_train.py::test_training_uses_no_vendor_gemm runs one earlier
                       in the same pytest process), then mode abi
-  profiler_then_loss  the same, then mode loss (round 5's failing sequence)
+  profiler_then_loss  the same, then mode loss
+  eager_then_loss     round 5's test_graphed_loss_matches_eager sequence: an eager Loss + backward
+                      on the default stream whose `loss` stays referenced (its autograd graph,
+                      AccumulateGrad nodes included, is kept alive), then the capture of mode loss
+  eager_freed_then_loss  the same eager step, its outputs dropped before the capture
 Prints one line per mode: "<mode> OK ..." or raises.
 """
+import faulthandler
 import os
 import sys
 
@@ -72,7 +77,7 @@ def mode_abi(dev):
         ops.resolved_schedule(n), n)
 
 
-def mode_loss(dev):
+def mode_loss(dev, eager_first=False):
     from models import model_res_sigmoid_multi as md
     net = md.NN(dev, 3)
     net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.make_weights(0).items()})
@@ -84,6 +89,12 @@ def mode_loss(dev):
     pts = torch.from_numpy(synth.make_pairs(E * n, 3, seed=90).reshape(E, n, 6)).to(dev)
     yo = torch.from_numpy(synth.make_speeds(E * n, seed=91).reshape(E, n, 2)).to(dev)
     params = [p for p in net.parameters() if p.requires_grad]
+    keep = None
+    if eager_first:   # as round 5's test: the eager step's loss is still referenced at capture
+        keep = model.Loss(pts, yo, Bt, 1.0, 1e-3)
+        keep[0].backward()
+        if eager_first == "freed":
+            keep = None
 
     def fn():
         for p in params:
@@ -117,13 +128,16 @@ def profiler_session(dev):
 
 
 def main(mode):
+    faulthandler.enable()   # a crash names the Python frame it happened in
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
     pre = ""
     if mode.startswith("profiler_then_"):
         pre = "after a profiler session (%d events); " % profiler_session(dev)
         mode = mode[len("profiler_then_"):]
-    msg = {"abi": mode_abi, "loss": mode_loss}[mode](dev)
+    msg = {"abi": mode_abi, "loss": mode_loss,
+           "eager_then_loss": lambda d: mode_loss(d, eager_first=True),
+           "eager_freed_then_loss": lambda d: mode_loss(d, eager_first="freed")}[mode](dev)
     print("%s OK: %s%s" % (sys.argv[1], pre, msg), flush=True)
 
 

@@ -188,8 +188,10 @@ def test_two_adamw_steps_vs_reference(name, dim):
     """Two Model.train inner steps from the fixture's state against the reference's recorded
     loss and parameters.  Adam's first update is lr·sign(g), so a weight whose gradient is
     resolved differently by two fp32 computations (the reference's CPU GEMMs, our split-bf16
-    MFMA ones) moves differently; each check therefore passes against the reference's fp32
-    values or against the exact (fp64) trajectory, with the same bound."""
+    MFMA ones) moves differently.  Every element is checked against the reference's fp32
+    values; an element outside that bound passes only where the reference's own value is off
+    the exact (fp64) trajectory's bound and ours is within it, and at most max(2, size/10^4)
+    such elements per tensor."""
     from pntf.train import AdamW
     dev = torch.device("cuda:0")
     case = name
@@ -228,25 +230,34 @@ def test_two_adamw_steps_vs_reference(name, dim):
             if name not in grads[0]:                 # encoder1.0: no gradient, unchanged
                 assert np.array_equal(got, f[k]), name
                 continue
-            # against the reference (δ: our step-1 gradient error vs its gradient) or against
-            # the fp64 trajectory (δ vs the exact gradient), elementwise the closer of the two
+            # the main assertion is against the reference's own fp32 values (δ: our step-1
+            # gradient error vs its gradient)
             g = np.minimum(np.abs(grads[0][name]), np.abs(grads[1][name]))
-            ok = np.zeros(got.shape, bool)
-            worst = None
-            for target, gref in ((f[k], f["grad:" + name]), (after64[name], g64[name])):
-                err = np.abs(got - target)
+
+            def bound_vs(gref):
                 delta = 2 * max(float(np.abs(grads[0][name] - gref).max()), 1e-12)
-                bound = 2e-6 + 8 * lr * delta / np.maximum(g, delta)
-                if worst is None:
-                    i = np.argmax(err - bound)
-                    worst = (float(err.flat[i]), float(bound.flat[i]))
-                    vs_ref = err <= bound
-                ok |= err <= bound
-            if not vs_ref.all():   # printed: which elements needed the exact trajectory
-                print("two-step %s %s: %d element(s) outside the bound of the reference's fp32 "
-                      "values, within that of the fp64 trajectory" % (case, name,
-                                                                       int((~vs_ref).sum())))
-            assert ok.all(), (name, int((~ok).sum()), worst)
+                return 2e-6 + 8 * lr * delta / np.maximum(g, delta)
+            err = np.abs(got - f[k])
+            b_ref = bound_vs(f["grad:" + name])
+            miss = err > b_ref
+            if miss.any():
+                # fp64 adjudication: allowed only where the reference's own fp32
+                # value is itself outside the bound of the exact (fp64) trajectory — an
+                # element whose update two fp32 computations resolved differently (Adam's
+                # first step is lr·sign(g)) — where ours is within it, and for a handful of
+                # elements per tensor
+                b64 = bound_vs(g64[name])
+                ref_off = np.abs(f[k] - after64[name]) > b64
+                ok64 = np.abs(got - after64[name]) <= b64
+                bad = miss & ~(ref_off & ok64)
+                i = int(np.argmax(err - b_ref))
+                assert not bad.any(), (name, int(bad.sum()), float(err.flat[i]),
+                                       float(b_ref.flat[i]))
+                allowed = max(2, got.size // 10000)
+                print("two-step %s %s: %d element(s) outside the reference bound, adjudicated "
+                      "against the fp64 trajectory (the reference itself is off it there; "
+                      "allowed %d)" % (case, name, int(miss.sum()), allowed))
+                assert miss.sum() <= allowed, (name, int(miss.sum()), allowed)
     assert np.array_equal(sd["encoder1.0.weight"].detach().cpu().numpy(), W["encoder1.0.weight"])
 
 

@@ -275,28 +275,67 @@ def test_frozen_layers_get_no_grad_and_others_match():
 
 
 @pytest.mark.gpu
-def test_epilogue_outputs_raise_on_backward_and_b_grad_raises():
-    """Model.Speed / Tau / TravelTimes / Gradient are fused epilogue kernels: differentiating
-    them raises instead of silently training nothing; so does asking for B's gradient."""
+@pytest.mark.parametrize("which", ["Speed", "Tau", "TravelTimes", "Gradient"])
+def test_epilogue_outputs_differentiable_vs_oracle(which):
+    """Model.Speed / Tau / TravelTimes / Gradient (models/model_res_sigmoid_multi.py:1173-1248)
+    are torch graphs of NN.out / out_grad / out_backgrad in the reference, so a loss on them
+    trains the weights.  With autograd recording and trainable weights the drop-in composes
+    them from its differentiable outputs (pntf.net compose_*): the values equal
+    the fused epilogue kernels' (no-grad path) to fp32 rounding, and the weight gradients of a
+    seeded weighted sum match the fp64 oracle (the composition's upstream gradient through
+    oracle.taylor_vjp) within GRAD_TOL of each tensor's largest gradient.  B's gradient still
+    raises."""
     from models import model_res_sigmoid_multi as md
+    from pntf import net as pnet
     from pntf.ops import PntfError
     dev = torch.device("cuda:0")
+    W = synth.make_weights(0)
     net = md.NN(dev, 3)
-    net.load_state_dict({k: torch.from_numpy(v) for k, v in synth.make_weights(0).items()})
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()})
     net.to(dev)
     m = md.Model(".", ".", 3, 2, device=dev)
     m.network = net
-    m.B = torch.from_numpy(synth.make_B(3)).to(dev)
-    xp = torch.from_numpy(synth.make_pairs(8, 3, seed=71)).to(dev)
-    for fn in (m.Speed, m.Tau, m.TravelTimes, lambda x: m.Gradient(x, m.B)):
-        with pytest.raises(PntfError):
-            fn(xp).sum().backward()
+    B = synth.make_B(3)
+    m.B = torch.from_numpy(B).to(dev)
+    n = 64
+    xp = synth.make_pairs(n, 3, seed=71)
+    x = torch.from_numpy(xp).to(dev)
+    fn = {"Speed": m.Speed, "Tau": m.Tau, "TravelTimes": m.TravelTimes,
+          "Gradient": lambda v: m.Gradient(v, m.B)}[which]
+    out = fn(x)
     with torch.no_grad():
-        assert m.Speed(xp).grad_fn is None            # inference: nothing attached
-    B = m.B.clone().requires_grad_(True)
-    t, d, _ = net.out_grad(xp, B)
+        fused = fn(x)
+    assert out.grad_fn is not None and fused.grad_fn is None
+    np.testing.assert_allclose(out.detach().cpu().numpy(), fused.cpu().numpy(), rtol=2e-5,
+                               atol=1e-6)
+    wt = np.random.default_rng(5).standard_normal(tuple(out.shape))
+    net.zero_grad()
+    (out * torch.from_numpy(wt).to(dev, out.dtype)).sum().backward()
+    # the oracle: τ, ∇τ in fp64 (out_backgrad's quirk for Gradient), the composition's upstream
+    # gradient by torch autograd in fp64 on the CPU, then the Taylor adjoint
+    compat = which == "Gradient"
+    (tau64, dtau64, _), _, _ = O.taylor_vjp(W, xp, B, dim=3, compat=compat, want_x=False)
+    t = torch.from_numpy(tau64).requires_grad_(True)
+    d = torch.from_numpy(dtau64).requires_grad_(True)
+    X = torch.from_numpy(xp.astype(np.float64))
+    comp = {"Speed": lambda: pnet.compose_speed(t, d, X, 3), "Tau": lambda: t,
+            "TravelTimes": lambda: pnet.compose_travel_time(t, X, 3),
+            "Gradient": lambda: pnet.compose_velocity(t, d, X, 3)}[which]()
+    (comp * torch.from_numpy(wt).reshape(comp.shape)).sum().backward()
+    gd = None if d.grad is None else d.grad.numpy()
+    _, g64, _ = O.taylor_vjp(W, xp, B, dim=3, g_tau=t.grad.numpy().reshape(-1), g_dtau=gd,
+                             compat=compat, want_x=False)
+    for k, p in net.named_parameters():
+        if k.startswith("encoder1.0"):
+            assert p.grad is None, k
+            continue
+        got, ref = p.grad.detach().cpu().numpy(), g64[k]
+        err = float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-30))
+        assert err < GRAD_TOL, (which, k, err)
+    Bg = m.B.clone().requires_grad_(True)
+    _, dd, _ = net.out_grad(x, Bg)
     with pytest.raises(PntfError):
-        d.sum().backward()
+        dd.sum().backward()
 
 
 @pytest.mark.gpu

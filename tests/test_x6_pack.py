@@ -26,7 +26,7 @@ SZ_BIAS = 128 + 4 * 128 + 128 + 6 * 256 + 128 + 128 + 4
 # forward direction: (float offset, out, in, columns sharing the weights) in the OFF_* order
 # the narrow (16x16x32) split copy of the forward direction (pntf_taylor.h pack_nx6_kernel)
 NX6_SZ = 3 * SZ_DIR // 2
-NX6_G = 8
+NX6_G = 16
 NAMES = ["encoder.0", "encoder.1", "encoder1.1", "encoder.2", "encoder1.2", "encoder.3",
          "generator.0", "generator1.0", "generator.1", "generator1.1", "generator.2",
          "generator1.2", "generator.3"]

@@ -81,10 +81,11 @@ __device__ __forceinline__ void wx6_split(const f32x16& v, int b, wbf16x8 (&s)[3
   }
 }
 // out tiles per group of an x6 layer: G accumulators of NC tiles live
-// PNTF_X6_ACC = 1 (round 6): the out bank is the accumulator and every layer's out tiles form
-// one group (xlayer below); the split copy is then in (kt, ot) step order for every layer
+// PNTF_X6_ACC = 1 (round 6, the default): the out bank is the accumulator and every layer's
+// out tiles form one group (xlayer below); the split copy is then in (kt, ot) step order for
+// every layer (0: round 5's engine, wlayer, and its order — diagnostic builds only)
 #ifndef PNTF_X6_ACC
-#define PNTF_X6_ACC 0
+#define PNTF_X6_ACC 1
 #endif
 #ifndef PNTF_X6_G1
 #define PNTF_X6_G1 (PNTF_X6_ACC ? 8 : 4)
@@ -1033,18 +1034,15 @@ struct XPend {
     if constexpr (!(PNTF_XNOPEND & (L::PF ? 2 : 1))) xdue<L, XSched<L>::STEPS + ST::value>(ly);
   }
 };
-// ... or all at once (before a phase that reads the whole bank)
+// ... or all at once (before a phase that reads the whole bank): the remaining virtual steps
+// in order, so that the σ prefetch ring never holds more than its NSLOT quads (issuing every
+// pending prefetch first overwrote slots before their chunks read them)
 template <class L>
 __device__ __forceinline__ void xflush(L& ly) {
   if constexpr (L::NCH > 0) {
-    static_for<0, L::NCH>([&](auto jj) {
-      constexpr int j = decltype(jj)::value;
-      if constexpr (L::PF && XSched<L>::P(j) >= XSched<L>::STEPS) ly.prefetch(j);
-    });
-    static_for<0, L::NCH>([&](auto jj) {
-      constexpr int j = decltype(jj)::value;
-      if constexpr (XSched<L>::E(j) >= XSched<L>::STEPS) ly.chunk(j);
-    });
+    constexpr int S0 = XSched<L>::STEPS, S1 = XSched<L>::E(L::NCH - 1) + 1;
+    if constexpr (S1 > S0)
+      static_for<S0, S1>([&](auto ss) { xdue<L, decltype(ss)::value>(ly); });
   }
 }
 
@@ -1214,6 +1212,11 @@ struct XBwd {
     for (int s = 0; s < 4; ++s) out[c * OT + t][4 * q + s] *= sg[j % NSLOT][s];
   }
 };
+
+// the split-bf16 fold in the kernels that stage the env-B table in LDS (the headline's); the
+// global-table instantiations keep the fp32 fold, whose registers fit beside their B pointers
+template <class BT>
+constexpr bool xfold() { return XFOLD && std::is_same<BT, WBt<true>>::value; }
 
 // ---------------------------------------------------------------- Fourier fold (x6 acc)
 // encoder[0]^T on split-bf16 MFMA fused with the Fourier Jacobian (:639-645).  Two passes; in
@@ -1568,6 +1571,20 @@ __device__ __forceinline__ void wide_backward_x(Ring& ring, Rsrc W, const PairIO
     XBwd<4, 4, 2, true, true> a1{Y, sc, WT_EBLK + 8, lane, {}};
     XBwd<4, 4, 2, false, true> b0{X, sc, WT_EBLK, lane, {}};
     XBwd<4, 4, 2, true, true> a0{Y, sc, WT_E0, lane, {}};
+#if defined(PNTF_XENCFLUSH)   // diagnostics: every reverse encoder layer finishes its chunks
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
+                                  WHead{WE + 3 * SZ_E * 4});
+    xflush(e3);
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, NoPre{},
+                                  WHead{WE + 2 * SZ_E * 4});
+    xflush(b1);
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
+                                  WHead{WE + 1 * SZ_E * 4});
+    xflush(a1);
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, NoPre{}, WHead{WE});
+    xflush(b0);
+    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE, X, lane, a0, NoPre{}, WFoldHead{});
+#else
     xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
                                   WHead{WE + 3 * SZ_E * 4});
     xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, XPend<decltype(e3)>{e3},
@@ -1576,16 +1593,17 @@ __device__ __forceinline__ void wide_backward_x(Ring& ring, Rsrc W, const PairIO
                                   WHead{WE + 1 * SZ_E * 4});
     xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, XPend<decltype(a1)>{a1},
                                   WHead{WE});
-    if constexpr (XFOLD)
+    if constexpr (xfold<BT>())
       xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE, X, lane, a0, XPend<decltype(b0)>{b0},
                                     WFoldXHead{});
     else
       xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE, X, lane, a0, XPend<decltype(b0)>{b0},
                                     WFoldHead{});
+#endif
     xflush(a0);
   }
 #endif
-  if constexpr (XFOLD) wide_fold_x<DIM>(ring, W, io, bt, X, Y, lane, ds, dg, after);
+  if constexpr (xfold<BT>()) wide_fold_x<DIM>(ring, W, io, bt, X, Y, lane, ds, dg, after);
   else wide_fold<DIM>(ring, W, io, bt, Y, lane, ds, dg, after);
 }
 #endif  // PNTF_WIDE_X6 && PNTF_X6_ACC

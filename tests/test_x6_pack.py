@@ -5,10 +5,11 @@
     copy, at the fragment the wide kernel's step order reads it from: per 32 x 32 step (ot, kt)
     and k block b, element i of lane l holds M[32 ot + (l & 31)][32 kt + (i & 3) + 16 b +
     8 (i >> 2) + 4 (l >> 5)], i.e. element i & 3 of fp32 fragment 2b + (i >> 2);
-  * step order: one-column layers (generator blocks, generator[-2]) in groups of 4 out tiles
-    (g, kt, o), fragments 3b + term; two-column layers (encoder[0], the encoder blocks,
-    encoder[-1]) per tile (ot, kt) in the first copy and block-major (g of 2 tiles, kt, b),
-    fragments 3o + term, in the second (OFF_X6BM);
+  * step order of the first copy (OFF_X6): every layer's out tiles in one group, steps
+    (kt, ot), fragments 3b + term, for the accumulate-in-bank engine (round 6; encoder[0]^T, the
+    Fourier fold, in two passes (p, kt, ot_local) of its sin/cos tiles 2p, 2p + 1); round 5's
+    groups of 4 / per tile with X6_ACC = False; the second copy (OFF_X6BM) block-major
+    (g of 2 tiles, kt, b), fragments 3o + term, for the two-column layers;
   * the three terms are the round-to-nearest-even bf16 splits x0 = bf16(x), x1 = bf16(x - x0),
     x2 = bf16(x - x0 - x1), bit for bit, and x0 + x1 + x2 == x exactly.
 """
@@ -41,12 +42,25 @@ def bf16_rne(x):
     return (r & 0xFFFFFFFF).astype(np.uint32).view(np.float32)
 
 
-def frag_index(gf, j, OT, KT, nc, b, bm):
+# The step order of the first copy follows the wide kernel's layer engine (pntf_wide.h):
+# PNTF_X6_ACC = 1 (round 6, the accumulate-in-bank xlayer): every layer's out tiles in one group,
+# steps (kt, ot); encoder[0]^T (the Fourier fold) in two passes of 4 out tiles.  Round 5's
+# engine: groups of 4 (one-column) / per tile (two-column layers).
+X6_ACC = True
+
+
+def frag_index(gf, j, OT, KT, nc, b, bm, fold=False):
     ot, kt = divmod(j, KT)
     base = gf - j
     if nc == 2 and bm:
         return (base + ((ot // 2) * KT + kt) * 2 + b) * 6 + (ot % 2) * 3
-    G = 1 if nc == 2 else 4
+    if X6_ACC and fold:
+        p, ol = (ot % 4) // 2, ((ot % 4) % 2) * 2 + ot // 4
+        return (base + (p * KT + kt) * 4 + ol) * 6 + 3 * b
+    if X6_ACC:
+        G = min(OT, 8) if nc == 1 else 4
+    else:
+        G = 1 if nc == 2 else 4
     return (base + (ot // G) * KT * G + kt * G + ot % G) * 6 + 3 * b
 
 
@@ -78,7 +92,7 @@ def test_x6_copies_match_their_definition():
                 for j in range(OT * KT):
                     gf = (d * SZ_DIR + m0) // 1024 + j
                     for b in range(2):
-                        fr = frag_index(gf, j, OT, KT, nc, b, bm)
+                        fr = frag_index(gf, j, OT, KT, nc, b, bm, fold=(d == 1 and m0 == 0))
                         for p in range(3):
                             assert np.array_equal(got[fr + p], want[gf, b, p]), (d, m0, j, b, p, bm)
                             seen[fr + p] += 1

@@ -20,6 +20,25 @@ namespace pntf {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Split-bf16 layers (pntf_wide.h wx6_split, pntf_taylor.h nx6_split): PNTF_X6_DOT = 1 takes
+// the residual x - bf16(x) of a split stage as one v_dot2c_f32_bf16 per element (x + p.lo·(-1)
+// + p.hi·0: the product is exact and so is the difference, an RNE residual being
+// representable) instead of an unpack and a subtract.
+#ifndef PNTF_X6_DOT
+#define PNTF_X6_DOT 0
+#endif
+typedef __bf16 x6bf16x2 __attribute__((ext_vector_type(2)));
+typedef float x6f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ x6f32x2 x6_resid(x6f32x2 x, x6bf16x2 p) {
+  // (-1, -0) and (-0, -1) as 32-bit literals: the plain (-1, 0) would be encoded as the inline
+  // constant -1.0, which the hardware does not read as the bf16 pair (-1, 0)
+  const x6bf16x2 nlo = __builtin_bit_cast(x6bf16x2, 0x8000bf80u), nhi = __builtin_bit_cast(x6bf16x2, 0xbf808000u);
+  x6f32x2 r;
+  r[0] = __builtin_amdgcn_fdot2_f32_bf16(p, nlo, x[0], false);
+  r[1] = __builtin_amdgcn_fdot2_f32_bf16(p, nhi, x[1], false);
+  return r;
+}
+
 constexpr int H = 128;              // hidden width (model_res_sigmoid_multi.py:134)
 constexpr int TILE = 16;            // pairs per wave
 constexpr int WAVES = 4;            // waves per workgroup (one per SIMD)

@@ -208,6 +208,10 @@ __device__ __forceinline__ void run_steps(Ring& ring, Rsrc r, int voff, AddrF ad
       for (int l = 0; l < NLN; ++l)
         ring.r[slot][l] = bload(r, voff, naddr(S + PF_STEPS - STEPS, l));
     }
+#ifdef PNTF_RING_AGPR   // the weight ring in the AGPR file (an MFMA reads its A operand there)
+#pragma unroll
+    for (int l = 0; l < RING_NL; ++l) asm("" : "+a"(ring.r[slot][l]));
+#endif
     body(st, a);
 #if PNTF_IGLP_CLUSTER == 1
     // One VALU cluster per step: beside f32 MFMAs every gap that carries vector work pays a

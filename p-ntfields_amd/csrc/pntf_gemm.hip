@@ -24,6 +24,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "pntf.h"
 #include "pntf_stamp.h"
 
@@ -601,15 +603,35 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// PNTF_X6_DOT = 1: each split stage's residual v - bf16(v) is one v_dot2c_f32_bf16 per
+// element (v + p.lo·(-1) + p.hi·0, exact), not an unpack and a subtract (pntf_common.h)
+#ifndef PNTF_X6_DOT
+#define PNTF_X6_DOT 0
+#endif
+__device__ __forceinline__ f32x2 x6_resid(f32x2 v, bf16x2 p) {
+  // (-1, -0) and (-0, -1) as 32-bit literals: the plain (-1, 0) would be encoded as the inline
+  // constant -1.0, which the hardware does not read as the bf16 pair (-1, 0)
+  const bf16x2 nlo = __builtin_bit_cast(bf16x2, 0x8000bf80u), nhi = __builtin_bit_cast(bf16x2, 0xbf808000u);
+  f32x2 r;
+  r[0] = __builtin_amdgcn_fdot2_f32_bf16(p, nlo, v[0], false);
+  r[1] = __builtin_amdgcn_fdot2_f32_bf16(p, nhi, v[1], false);
+  return r;
+}
 // three-term RNE split of 8 fp32 (k order of the bf16 operand lane: 8 consecutive k)
 __device__ __forceinline__ void x6_split(const f32x4& a, const f32x4& b, bf16x8 (&s)[3]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const f32x2 v = i < 2 ? f32x2{a[2 * i], a[2 * i + 1]} : f32x2{b[2 * i - 4], b[2 * i - 3]};
     const bf16x2 p0 = __builtin_convertvector(v, bf16x2);
+#if PNTF_X6_DOT
+    const f32x2 r1 = x6_resid(v, p0);
+    const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
+    const f32x2 r2 = x6_resid(r1, p1);
+#else
     const f32x2 r1 = v - __builtin_convertvector(p0, f32x2);
     const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
     const f32x2 r2 = r1 - __builtin_convertvector(p1, f32x2);
+#endif
     const bf16x2 p2 = __builtin_convertvector(r2, bf16x2);
     s[0][2 * i] = p0[0]; s[0][2 * i + 1] = p0[1];
     s[1][2 * i] = p1[0]; s[1][2 * i + 1] = p1[1];
@@ -687,6 +709,8 @@ template <int KC, int NC, bool ACC, int V = 3>
 __global__ __launch_bounds__(256, PNTF_X6_WPS) void panel_x6_kernel(PanelArgs g) {
   PNTF_CLOCK_SCOPE;
   constexpr int KB = KC / 16, QK = KC / 8, CG = x6_cg(KC, NC), TG = CG / 32, NG = NC / CG;
+  // the LDS-transposed store flushes a block after every odd tile
+  static_assert(!PNTF_X6_TSTORE || TG % 2 == 0, "PNTF_X6_TSTORE needs an even tile count per group");
   constexpr int FR = TG * KB * 3;   // 1 KiB fragments per group
   static_assert(KB >= 4, "C prefetch distance");
   __shared__ bf16x8 lw[FR * 64];
@@ -1896,14 +1920,17 @@ bool panel_shape(int64_t N, int64_t K) {
 // PNTF_GEMM_PANEL: 0 = off, 1 = the register-stream panel kernel, 2 = the LDS one (fp32 MFMA),
 // 3 (default) = the split-bf16 LDS one (panel_x6_kernel).
 // pntf_tt_set_panel_mode overrides it (tests and A/B probes).
-int g_panel_mode = -1;
-int panel_mode() {
-  if (g_panel_mode < 0) {
-    const char* e = getenv("PNTF_GEMM_PANEL");
-    g_panel_mode = e && e[0] >= '0' && e[0] <= '8' ? e[0] - '0' : 3;
-  }
-  return g_panel_mode;
+// (set once from the environment, thread-safely; then only by pntf_tt_set_panel_mode)
+std::atomic<int> g_panel_mode{-1};
+int mode_from_env(std::atomic<int>& m, const char* var, char hi, int dflt) {
+  int v = m.load(std::memory_order_relaxed);
+  if (v >= 0) return v;
+  const char* e = getenv(var);
+  int expect = -1;
+  m.compare_exchange_strong(expect, e && e[0] >= '0' && e[0] <= hi ? e[0] - '0' : dflt);
+  return m.load(std::memory_order_relaxed);
 }
+int panel_mode() { return mode_from_env(g_panel_mode, "PNTF_GEMM_PANEL", '8', 3); }
 // work floats of the packed weight: fp32 fragments, or three bf16 terms (1.5x)
 size_t panel_pack_floats(int64_t N, int64_t K) {
   return panel_mode() >= 3 ? (size_t)(K * N * 3 / 2) : (size_t)(K * N);
@@ -1917,14 +1944,8 @@ bool wgrad_shape(int64_t M, int64_t N) {
 }
 // PNTF_GEMM_WGRAD: 0 = the LDS-tiled kernel, 1 = wgrad_kernel (fp32 MFMA), 2 (default) =
 // wgrad_x6_kernel (split bf16); pntf_tt_set_wgrad_mode overrides it.
-int g_wgrad_mode = -1;
-int wgrad_mode() {
-  if (g_wgrad_mode < 0) {
-    const char* e = getenv("PNTF_GEMM_WGRAD");
-    g_wgrad_mode = e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
-  }
-  return g_wgrad_mode;
-}
+std::atomic<int> g_wgrad_mode{-1};
+int wgrad_mode() { return mode_from_env(g_wgrad_mode, "PNTF_GEMM_WGRAD", '2', 2); }
 bool wgrad_enabled() { return wgrad_mode() != 0; }
 // Refill scheme per tile count: the two-buffer burst for the 256 x 256 gradients (T = 4:
 // 206 vs 215 µs at 9 x 20 000 rows), the per-slot ring for T = 1, 2 (64 vs 67, 103 vs 106 µs;
@@ -1955,7 +1976,9 @@ size_t pntf_tt_gemm_work_floats(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const int64_t s = splits_for(M, N, K);
   const size_t split = s > 1 ? (size_t)(s * M * N) : 0;
-  const size_t packed = panel_shape(N, K) ? panel_pack_floats(N, K) : 0;
+  // the largest packed layout (the split-bf16 one, 1.5 K·N) whatever the current panel mode,
+  // so a buffer sized here stays large enough after pntf_tt_set_panel_mode
+  const size_t packed = panel_shape(N, K) ? (size_t)(K * N * 3 / 2) : 0;
   const size_t wgrad = wgrad_shape(M, N) ? (size_t)((wgrad_splits(M, N, K) + 7) * M * N) : 0;
   const size_t big = split > packed ? split : packed;
   return big > wgrad ? big : wgrad;

@@ -76,9 +76,15 @@ __device__ __forceinline__ void nx6_split(const f32x4& lo, const f32x4& hi, nbf1
     nf32x2 x = i < 2 ? nf32x2{lo[2 * i], lo[2 * i + 1]} : nf32x2{hi[2 * i - 4], hi[2 * i - 3]};
     asm volatile("" : "+v"(x));   // split here, not hoisted into a whole split bank
     const nbf16x2 p0 = __builtin_convertvector(x, nbf16x2);
+#if PNTF_X6_DOT
+    const nf32x2 r1 = x6_resid(x, p0);
+    const nbf16x2 p1 = __builtin_convertvector(r1, nbf16x2);
+    const nf32x2 r2 = x6_resid(r1, p1);
+#else
     const nf32x2 r1 = x - __builtin_convertvector(p0, nf32x2);
     const nbf16x2 p1 = __builtin_convertvector(r1, nbf16x2);
     const nf32x2 r2 = r1 - __builtin_convertvector(p1, nf32x2);
+#endif
     const nbf16x2 p2 = __builtin_convertvector(r2, nbf16x2);
     s[0][2 * i] = p0[0]; s[0][2 * i + 1] = p0[1];
     s[1][2 * i] = p1[0]; s[1][2 * i + 1] = p1[1];

@@ -71,9 +71,15 @@ __device__ __forceinline__ void wx6_split(const f32x16& v, int b, wbf16x8 (&s)[3
     s[0][2 * i + 1] = s[1][2 * i + 1] = s[2][2 * i + 1] = p0[1];
     continue;
 #endif
+#if PNTF_X6_DOT
+    const wf32x2 r1 = x6_resid(x, p0);
+    const wbf16x2 p1 = __builtin_convertvector(r1, wbf16x2);
+    const wf32x2 r2 = x6_resid(r1, p1);
+#else
     const wf32x2 r1 = x - __builtin_convertvector(p0, wf32x2);
     const wbf16x2 p1 = __builtin_convertvector(r1, wbf16x2);
     const wf32x2 r2 = r1 - __builtin_convertvector(p1, wf32x2);
+#endif
     const wbf16x2 p2 = __builtin_convertvector(r2, wbf16x2);
     s[0][2 * i] = p0[0]; s[0][2 * i + 1] = p0[1];
     s[1][2 * i] = p1[0]; s[1][2 * i + 1] = p1[1];
@@ -1067,6 +1073,7 @@ __device__ __forceinline__ void xagpr(f32x16& t) {
   asm("" : "+a"(t));
 #endif
 }
+__device__ __forceinline__ void xvgpr(f32x16& t) { asm("" : "+v"(t)); }
 // Each input tile is split once per layer here, so nothing invites the compiler to keep a
 // split bank live; the opaque copy of wx6_split (round 5) only costs moves (PNTF_XOPQ = 1 keeps it)
 #ifndef PNTF_XOPQ
@@ -1082,7 +1089,7 @@ constexpr bool XOPQ = PNTF_XOPQ;
 // bank `in` (c·KT + kt).  ly.init(ot) starts out tile ot at kt = 0 (bias MFMA / residual /
 // zero); ly's chunks run as above; pre(st) runs first in every step (the previous layer's
 // pending chunks, loads for the next layer).
-template <int OT, int KT, int NC, int SITE, class L, class PreF, class NextF>
+template <int OT, int KT, int NC, int SITE, bool IN_X, class L, class PreF, class NextF>
 __device__ __forceinline__ void xlayer(Ring& ring, Rsrc W, int wbase, f32x16 (&in)[8],
                                        int lane, L& ly, PreF pre, NextF naddr) {
   static_assert(NC * KT <= 8 && NC * OT <= 8, "bank size");
@@ -1109,13 +1116,28 @@ __device__ __forceinline__ void xlayer(Ring& ring, Rsrc W, int wbase, f32x16 (&i
           for (int c = 0; c < NC; ++c)
             ly.out[c * OT + ot] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs[p][c][b],
                                           ly.out[c * OT + ot]);
+#if PNTF_XAGPR != 3
 #pragma unroll
         for (int c = 0; c < NC; ++c) xagpr(ly.out[c * OT + ot]);
+#endif
 #if PNTF_XAGPR == 2
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
           xagpr(in[t]);
           xagpr(ly.out[t]);
+        }
+#elif PNTF_XAGPR == 3
+        // bank X in the VGPR file, bank Y in the AGPR file: a layer reading X splits without
+        // AGPR reads, one accumulating into X runs its epilogue chunks without AGPR moves
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          if constexpr (IN_X) {
+            xvgpr(in[t]);
+            xagpr(ly.out[t]);
+          } else {
+            xagpr(in[t]);
+            xvgpr(ly.out[t]);
+          }
         }
 #endif
         if constexpr (PIPE && kt + 1 < KT) {
@@ -1251,8 +1273,16 @@ __device__ __forceinline__ void wide_fold_x(Ring& ring, Rsrc W, const PairIO& io
 #pragma unroll
           for (int c = 0; c < 2; ++c)
             X[c * 4 + otl] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs[c][b], X[c * 4 + otl]);
+#if PNTF_XAGPR == 3
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          xvgpr(X[t]);
+          xagpr(Y[t]);
+        }
+#else
 #pragma unroll
         for (int c = 0; c < 2; ++c) xagpr(X[c * 4 + otl]);
+#endif
 #if PNTF_XAGPR == 2
 #pragma unroll
         for (int t = 0; t < 8; ++t) xagpr(Y[t]);   // both banks in the AGPR file (as xlayer)
@@ -1340,8 +1370,17 @@ __device__ __forceinline__ float wide_forward_x(Ring& ring, Rsrc W, const PairIO
 #pragma unroll
             for (int c = 0; c < 2; ++c)
               X[c * 4 + ot] = wx6_mma(a[3 * b], a[3 * b + 1], a[3 * b + 2], xs[c][b], X[c * 4 + ot]);
+#if PNTF_XAGPR == 3
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            xvgpr(X[t]);
+            if (kt >= 4 || t % 4 < kt) xagpr(Y[t]);
+          }
+#endif
+#if PNTF_XAGPR != 3
 #pragma unroll
           for (int c = 0; c < 2; ++c) xagpr(X[c * 4 + ot]);
+#endif
 #if PNTF_XAGPR == 2
 #pragma unroll
           for (int t = 0; t < 8; ++t) {
@@ -1364,24 +1403,24 @@ __device__ __forceinline__ float wide_forward_x(Ring& ring, Rsrc W, const PairIO
     XFwdAct<4, 4, 2, false, GRAD> a1{Y, sc, WT_EBLK + 16, lane, {}, wl, 0.f};
     XFwdAct<4, 4, 2, true, GRAD> b1{X, sc, WT_EBLK + 24, lane, {}, wl, 0.f};
     XFwdLin<4, 4, 2> e3{Y, {}};
-    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WE, X, lane, a0,
+    xlayer<4, 4, 2, SITE_FWD_ENC, true>(ring, W, WE, X, lane, a0,
                                   both(XPend<decltype(e0)>{e0},
                                        at<0>([&] { b0.bc.load(W, lane, B_EBLK + 128); })),
                                   WHead{WE + SZ_E * 4});
-    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WE + SZ_E * 4, Y, lane, b0,
+    xlayer<4, 4, 2, SITE_FWD_ENC, false>(ring, W, WE + SZ_E * 4, Y, lane, b0,
                                   both(XPend<decltype(a0)>{a0},
                                        at<0>([&] { a1.bc.load(W, lane, B_EBLK + 256); })),
                                   WHead{WE + 2 * SZ_E * 4});
-    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
+    xlayer<4, 4, 2, SITE_FWD_ENC, true>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1,
                                   both(XPend<decltype(b0)>{b0},
                                        at<0>([&] { b1.bc.load(W, lane, B_EBLK + 384); })),
                                   WHead{WE + 3 * SZ_E * 4});
-    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
+    xlayer<4, 4, 2, SITE_FWD_ENC, false>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1,
                                   both(XPend<decltype(a1)>{a1},
                                        at<0>([&] { e3.bc.load(W, lane, B_E3); })),
                                   WHead{WF + OFF_E3 * 4});
     // ---- encoder[-1] (:234) -> Y (zs = Y[0..3], zg = Y[4..7])
-    xlayer<4, 4, 2, SITE_FWD_ENC>(ring, W, WF + OFF_E3 * 4, X, lane, e3, XPend<decltype(b1)>{b1},
+    xlayer<4, 4, 2, SITE_FWD_ENC, true>(ring, W, WF + OFF_E3 * 4, X, lane, e3, XPend<decltype(b1)>{b1},
                                   WHead{WF + OFF_GBLK * 4});
   }
 
@@ -1408,7 +1447,7 @@ __device__ __forceinline__ float wide_forward_x(Ring& ring, Rsrc W, const PairIO
   XFwdAct<8, 8, 1, false, GRAD> ga{Y, sc, WT_GBLK, lane, {}, wl, 0.f};
   XFwdAct<8, 8, 1, true, GRAD> gb{X, sc, WT_GBLK + 8, lane, {}, wl, 0.f};
   ga.bc.load(W, lane, B_GBLK);
-  xlayer<8, 8, 1, SITE_FWD_GEN>(ring, W, WF + OFF_GBLK * 4, X, lane, ga,
+  xlayer<8, 8, 1, SITE_FWD_GEN, true>(ring, W, WF + OFF_GBLK * 4, X, lane, ga,
                                 at<0>([&] { gb.bc.load(W, lane, B_GBLK + 256); }),
                                 WHead{WF + (OFF_GBLK + SZ_G) * 4});
 #pragma unroll 1
@@ -1418,12 +1457,12 @@ __device__ __forceinline__ float wide_forward_x(Ring& ring, Rsrc W, const PairIO
     const int wn = opaque(WF + (OFF_GBLK + (2 * i + 3) * SZ_G) * 4);
     const int ba = opaque(B_GBLK + (2 * i + 2) * 256);
     gb.sc0 = opaque(WT_GBLK + 16 * i + 8);
-    xlayer<8, 8, 1, SITE_FWD_GEN>(ring, W, wb, Y, lane, gb,
+    xlayer<8, 8, 1, SITE_FWD_GEN, false>(ring, W, wb, Y, lane, gb,
                                   both(XPend<decltype(ga)>{ga},
                                        at<0>([&] { ga.bc.load(W, lane, ba); })),
                                   WHead{wa});
     ga.sc0 = opaque(WT_GBLK + 16 * i + 16);
-    xlayer<8, 8, 1, SITE_FWD_GEN>(ring, W, wa, X, lane, ga,
+    xlayer<8, 8, 1, SITE_FWD_GEN, true>(ring, W, wa, X, lane, ga,
                                   both(XPend<decltype(gb)>{gb},
                                        at<0>([&] { gb.bc.load(W, lane, ba + 256); })),
                                   WHead{wn});
@@ -1431,11 +1470,11 @@ __device__ __forceinline__ float wide_forward_x(Ring& ring, Rsrc W, const PairIO
   // ---- generator block 2's second layer, then generator[-2] + act (:251-252) -> Y[0..3]
   XFwdAct<4, 8, 1, false, GRAD, true> g3{Y, sc, WL_G3, lane, {}, wl, 0.f};
   gb.sc0 = WT_GBLK + 16 * 2 + 8;
-  xlayer<8, 8, 1, SITE_FWD_GEN>(ring, W, WF + (OFF_GBLK + 5 * SZ_G) * 4, Y, lane, gb,
+  xlayer<8, 8, 1, SITE_FWD_GEN, false>(ring, W, WF + (OFF_GBLK + 5 * SZ_G) * 4, Y, lane, gb,
                                 both(XPend<decltype(ga)>{ga},
                                      at<0>([&] { g3.bc.load(W, lane, B_G3); })),
                                 WHead{WF + OFF_G3 * 4});
-  xlayer<4, 8, 1, SITE_FWD_GEN>(ring, W, WF + OFF_G3 * 4, X, lane, g3, XPend<decltype(gb)>{gb},
+  xlayer<4, 8, 1, SITE_FWD_GEN, true>(ring, W, WF + OFF_G3 * 4, X, lane, g3, XPend<decltype(gb)>{gb},
                                 after);
   xflush(g3);
   // ---- head generator[-1] + sigmoid(0.1 y) (:254-255)
@@ -1505,13 +1544,13 @@ __device__ __forceinline__ void wide_backward_x(Ring& ring, Rsrc W, const PairIO
 #else
   // du = G3^T dv ⊙ σ10(y2 of generator block 2) -> X   (G3^T: 256 x 128, OT 8, KT 4)
   XBwd<8, 4, 1, false, true> l3{X, sc, WT_GBLK + 16 * 2 + 8, lane, {}};
-  xlayer<8, 4, 1, SITE_BWD_GEN>(ring, W, WB + OFF_G3 * 4, Y, lane, l3, NoPre{},
+  xlayer<8, 4, 1, SITE_BWD_GEN, false>(ring, W, WB + OFF_G3 * 4, Y, lane, l3, NoPre{},
                                 WHead{WB + (OFF_GBLK + 5 * SZ_G) * 4});
   // ---- generator blocks, reverse (:615-618), rotated: lb_2; (la_i, lb_{i-1}) for i = 2, 1;
   // la_0 (no σ: it hands over to encoder[-1]^T)
   XBwd<8, 8, 1, false, true> lb{Y, sc, WT_GBLK + 16 * 2, lane, {}};
   XBwd<8, 8, 1, true, true> la{X, sc, 0, lane, {}};
-  xlayer<8, 8, 1, SITE_BWD_GEN>(ring, W, WB + (OFF_GBLK + 5 * SZ_G) * 4, X, lane, lb,
+  xlayer<8, 8, 1, SITE_BWD_GEN, true>(ring, W, WB + (OFF_GBLK + 5 * SZ_G) * 4, X, lane, lb,
                                 XPend<decltype(l3)>{l3}, WHead{WB + (OFF_GBLK + 4 * SZ_G) * 4});
 #pragma unroll 1
   for (int i = 2; i >= 1; --i) {
@@ -1520,14 +1559,14 @@ __device__ __forceinline__ void wide_backward_x(Ring& ring, Rsrc W, const PairIO
     const int wn = opaque(WB + (OFF_GBLK + (2 * i - 2) * SZ_G) * 4);
     // du = G_i^T da + dr, then ⊙ σ10(y2_{i-1})
     la.mul0 = opaque(WT_GBLK + 16 * (i - 1) + 8);
-    xlayer<8, 8, 1, SITE_BWD_GEN>(ring, W, wa, Y, lane, la, XPend<decltype(lb)>{lb}, WHead{wb});
+    xlayer<8, 8, 1, SITE_BWD_GEN, false>(ring, W, wa, Y, lane, la, XPend<decltype(lb)>{lb}, WHead{wb});
     // da = (G1_{i-1}^T dr) ⊙ σ10(y1_{i-1}) -> Y
     lb.mul0 = opaque(WT_GBLK + 16 * (i - 1));
-    xlayer<8, 8, 1, SITE_BWD_GEN>(ring, W, wb, X, lane, lb, XPend<decltype(la)>{la}, WHead{wn});
+    xlayer<8, 8, 1, SITE_BWD_GEN, true>(ring, W, wb, X, lane, lb, XPend<decltype(la)>{la}, WHead{wn});
   }
   {
     XBwd<8, 8, 1, true, false> l0{X, sc, 0, lane, {}};
-    xlayer<8, 8, 1, SITE_BWD_GEN>(ring, W, WB + OFF_GBLK * 4, Y, lane, l0,
+    xlayer<8, 8, 1, SITE_BWD_GEN, false>(ring, W, WB + OFF_GBLK * 4, Y, lane, l0,
                                   XPend<decltype(lb)>{lb}, WHead{WB + OFF_E3 * 4});
   }
 #endif
@@ -1572,32 +1611,32 @@ __device__ __forceinline__ void wide_backward_x(Ring& ring, Rsrc W, const PairIO
     XBwd<4, 4, 2, false, true> b0{X, sc, WT_EBLK, lane, {}};
     XBwd<4, 4, 2, true, true> a0{Y, sc, WT_E0, lane, {}};
 #if defined(PNTF_XENCFLUSH)   // diagnostics: every reverse encoder layer finishes its chunks
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
+    xlayer<4, 4, 2, SITE_BWD_ENC, true>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
                                   WHead{WE + 3 * SZ_E * 4});
     xflush(e3);
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, NoPre{},
+    xlayer<4, 4, 2, SITE_BWD_ENC, false>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, NoPre{},
                                   WHead{WE + 2 * SZ_E * 4});
     xflush(b1);
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
+    xlayer<4, 4, 2, SITE_BWD_ENC, true>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, NoPre{},
                                   WHead{WE + 1 * SZ_E * 4});
     xflush(a1);
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, NoPre{}, WHead{WE});
+    xlayer<4, 4, 2, SITE_BWD_ENC, false>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, NoPre{}, WHead{WE});
     xflush(b0);
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE, X, lane, a0, NoPre{}, WFoldHead{});
+    xlayer<4, 4, 2, SITE_BWD_ENC, true>(ring, W, WE, X, lane, a0, NoPre{}, WFoldHead{});
 #else
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
+    xlayer<4, 4, 2, SITE_BWD_ENC, true>(ring, W, WB + OFF_E3 * 4, X, lane, e3, NoPre{},
                                   WHead{WE + 3 * SZ_E * 4});
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, XPend<decltype(e3)>{e3},
+    xlayer<4, 4, 2, SITE_BWD_ENC, false>(ring, W, WE + 3 * SZ_E * 4, Y, lane, b1, XPend<decltype(e3)>{e3},
                                   WHead{WE + 2 * SZ_E * 4});
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, XPend<decltype(b1)>{b1},
+    xlayer<4, 4, 2, SITE_BWD_ENC, true>(ring, W, WE + 2 * SZ_E * 4, X, lane, a1, XPend<decltype(b1)>{b1},
                                   WHead{WE + 1 * SZ_E * 4});
-    xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, XPend<decltype(a1)>{a1},
+    xlayer<4, 4, 2, SITE_BWD_ENC, false>(ring, W, WE + 1 * SZ_E * 4, Y, lane, b0, XPend<decltype(a1)>{a1},
                                   WHead{WE});
     if constexpr (xfold<BT>())
-      xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE, X, lane, a0, XPend<decltype(b0)>{b0},
+      xlayer<4, 4, 2, SITE_BWD_ENC, true>(ring, W, WE, X, lane, a0, XPend<decltype(b0)>{b0},
                                     WFoldXHead{});
     else
-      xlayer<4, 4, 2, SITE_BWD_ENC>(ring, W, WE, X, lane, a0, XPend<decltype(b0)>{b0},
+      xlayer<4, 4, 2, SITE_BWD_ENC, true>(ring, W, WE, X, lane, a0, XPend<decltype(b0)>{b0},
                                     WFoldHead{});
 #endif
     xflush(a0);

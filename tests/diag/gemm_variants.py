@@ -7,6 +7,7 @@ import sys
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+FIRST = {}   # outputs of the first build named, to report each later build's bitwise difference
 
 
 def timeit(fn, reps=10):
@@ -27,6 +28,7 @@ def main(names, pairs=20000, check=True):
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     shapes = (("gen", 13 * pairs, 256, 256), ("enc", 14 * pairs, 128, 128),
               ("enc0", 14 * pairs, 256, 128))
+    torch.manual_seed(0)
     for name in names:
         # "<lib>@<mode>": libgemm_<lib>.so with pntf_tt_set_panel_mode(<mode>)
         lname, _, mode = name.partition("@")
@@ -67,6 +69,13 @@ def main(names, pairs=20000, check=True):
             torch.cuda.synchronize()
             assert not check or (GX - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
             res[tag + "_bwdw"] = round(fl / timeit(run(GW, G, X, 1, 0, N, K, rows)), 1)
+            torch.cuda.synchronize()
+            for t, o in (("fwd", Y), ("bwdx", GX), ("bwdw", GW)):
+                k = tag + "_" + t
+                if k not in FIRST:
+                    FIRST[k] = o.clone()
+                else:
+                    res[k + "_maxdiff_vs_first"] = (o - FIRST[k]).abs().max().item()
         print(name, res, flush=True)
 
 

@@ -166,7 +166,9 @@ def test_wide_env_table_in_lds_matches_global(packed, dev, dim, fit):
     """The wide kernels stage the env-B table in LDS when n_env · dim · 128 floats fit in
     WBL_FLOATS (pntf_common.h; 13 envs at dim 3, 6 at dim 6) and read it from global memory
     otherwise.  Same pairs and env ids, the table padded by one more environment so that it no
-    longer fits: bitwise equal results, at the limit and one below it."""
+    longer fits, at the limit and one below it: τ bitwise equal; ∇τ equal to fp32 rounding (the
+    LDS-table instantiation — the headline's — runs the Fourier fold on split-bf16 MFMA, the
+    global-table one on fp32 MFMA: pntf_wide.h xfold, round 6), per pair within 1e-5."""
     n = 2 * 32 * 257
     xp = T(synth.make_pairs(n, dim, seed=41), dev)
     for E in (fit, fit - 1):
@@ -174,8 +176,11 @@ def test_wide_env_table_in_lds_matches_global(packed, dev, dim, fit):
         env = T(synth.make_env_ids(n, E, contiguous=False, seed=E), dev, torch.int32)
         t_l, d_l = ops.tau_grad(packed, xp, T(Bt[:E], dev), env, dim=dim, schedule="wide_tile")
         t_g, d_g = ops.tau_grad(packed, xp, T(Bt, dev), env, dim=dim, schedule="wide_tile")
-        assert torch.equal(t_l, t_g) and torch.equal(d_l, d_g)
-        assert torch.isfinite(t_l).all()
+        assert torch.equal(t_l, t_g)
+        dl, dg = d_l.double(), d_g.double()
+        r = (dl - dg).norm(dim=1) / dg.norm(dim=1).clamp_min(1e-30)
+        assert float(r.max()) < 1e-5, float(r.max())
+        assert torch.isfinite(t_l).all() and torch.isfinite(d_l).all()
 
 
 def test_coincident_endpoints(packed, dev, W):
@@ -478,8 +483,10 @@ def test_headline_1m_sample_vs_fp64_oracle(packed, dev, W):
                          dim=3, schedule="wave_tile")
     e_f32 = max_rel(dw.cpu().numpy(), do, floor)
     print("headline dtau componentwise vs fp64: HIP %.2e, fp32 reference %.2e, fp32-MFMA "
-          "wave-tile kernel %.2e" % (e_hip, e_ref, e_f32))
-    assert e_hip <= max(1e-4, e_ref)
+          "wave-tile kernel %.2e (HIP / reference %.3f)" % (e_hip, e_ref, e_f32, e_hip / e_ref))
+    # measured headroom: 1.77e-4 against the reference's 2.02e-4 (0.876) with the
+    # split-bf16 layers of round 6; held to 0.95 so that a change eating the margin fails here
+    assert e_hip <= 0.95 * max(1e-4, e_ref)
 
 
 def test_c4_shape_sharded_on_one_gpu(packed, dev, W):

@@ -67,6 +67,8 @@ def main(only=None, wlib="libperf_wstamp.so"):
     lib = ctypes.CDLL(os.path.join(HERE, wlib))
     n = 1 << 20
     xp = torch.from_numpy(synth.make_pairs(n, 3, seed=1000)).to(dev)
+    if os.environ.get("PERF_DATA") == "same":   # every pair the same: lanes carry equal values
+        xp = xp[:1].expand(n, -1).contiguous()
     B = torch.from_numpy(synth.make_B(3, seed=1)).to(dev).unsqueeze(0).contiguous()
     t, d = torch.empty(n, device=dev), torch.empty(n, 6, device=dev)
     ws = torch.empty(cus * 4 * 96 * 1024 * 4, dtype=torch.uint8, device=dev)

@@ -327,6 +327,10 @@ int pntf_tt_set_panel_mode(int mode);
  * PNTF_GEMM_WGRAD in the environment): 0 = the LDS-tiled kernel, 1 = the fp32-MFMA wgrad
  * kernel, 2 (default) = the split-bf16 one; returns the previous mode. */
 int pntf_tt_set_wgrad_mode(int mode);
+/* The kernel of pntf_tt_linear_bwd (PNTF_GEMM_BWD in the environment): 0 = fp32 MFMA, 1
+ * (default) = split bf16 (the x6 GEMM of pntf_tt_gemm with the act adjoint as its epilogue);
+ * returns the previous mode, leaves it unchanged for a mode outside 0..1. */
+int pntf_tt_set_bwd_mode(int mode);
 
 /* One Linear of the Taylor tape with its bias, residual and act_laplace fused (the forward
  * GEMM of pntf_tt_gemm followed by pntf_tt_act_fwd, in one kernel; :663-691, :744/:828):

@@ -1591,6 +1591,181 @@ __global__ __launch_bounds__(256, 1) void panel_bwd_coop_kernel(BwdArgs g) {
   }
 }
 
+// The same fused input gradient + act adjoint on the split-bf16 MFMA (round 6,
+// `panel_bwd_x6_kernel`, bwd mode 1): gY·W as panel_x6_kernel computes it (three-term splits of
+// both operands, six v_mfma_f32_32x32x16_bf16 per 32 x 32 x 16 block, per-order accumulators
+// summed smallest first), then the epilogue of panel_bwd_coop_kernel above.  A workgroup holds
+// the pre-split W of a 64-column group in LDS (96 KiB at KC = 256); wave w owns out tile w & 1
+// of the group and point blocks 2·wg + (w >> 1) + 2·nwg·i, so two waves share each block's panel
+// rows (the second read hits the CU's caches).  Per wave: the 32-row panel of one plane (QK
+// float4 registers, the next plane's loaded behind the current one's MFMAs, as in
+// panel_x6_kernel), three accumulators and the epilogue state (σ, g_L, acc₀) of one out tile.
+// Bias partials: row 2·wg + (w >> 1) of `partial`, the wave's 32 columns.
+template <int KC, int NC>
+__global__ __launch_bounds__(256, 1) void panel_bwd_x6_kernel(BwdArgs g) {
+  constexpr int KB = KC / 16, QK = KC / 8, CG = 64, NG = NC / CG, FR = 2 * KB * 3;
+  __shared__ bf16x8 lw[FR * 64];
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int grp = 0, wg = blockIdx.x, nwg = gridDim.x;
+  if constexpr (NG > 1) {
+    const int x = blockIdx.x & 7, s = blockIdx.x >> 3;
+    grp = s % NG;
+    wg = (s / NG) * 8 + x;
+    nwg = gridDim.x / NG;
+  }
+  {
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(g.P) + (int64_t)grp * FR * 64;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < FR * 64; i += 256) lw[i] = src[i];
+  }
+  __syncthreads();
+  const int t = w & 1, pb = w >> 1;
+  const int c0 = CG * grp + 32 * t;   // the wave's 32 out columns
+  f32x4 bsum[4];
+#pragma unroll
+  for (int Q = 0; Q < 4; ++Q) bsum[Q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nblk = (g.M + 31) / 32, bstride = 2 * (int64_t)nwg;
+  int64_t blk = 2 * (int64_t)wg + pb;
+  if (blk < nblk) {
+    const int R = g.R, ndir = g.ndir, nl = g.nl, GK = nl ? ndir / nl : 1;
+    const bool has_res = g.res != nullptr;
+    // plane at sequence position i: per group l its L plane then its GK J planes; value last
+    auto plane_of = [&](int i) {
+      if (i == R - 1) return 0;
+      const int l = i / (GK + 1), k = i % (GK + 1);
+      return k == 0 ? 1 + ndir + l : 1 + l * GK + (k - 1);
+    };
+    auto win = [&](const float* base, int ld, int64_t b, int r) {
+      const int64_t rows = g.M - 32 * b;
+      return pg_rsrc(base + ((int64_t)r * g.M + 32 * b) * ld, (rows < 32 ? rows : 32) * ld * 4);
+    };
+    // lane (j, h): panel row j, k = 16 kb + 8 h .. +7 as two float4 (x[2 kb], x[2 kb + 1]);
+    // out row j, columns c0 + 8 Q + 4 h .. +3
+    const int va = (j * KC + 8 * h) * 4, vc = (j * NC + 4 * h) * 4;
+    f32x4 x[QK];
+    {
+      const Rsrc ra = win(g.A, KC, blk, plane_of(0));
+#pragma unroll
+      for (int q = 0; q < QK; ++q) x[q] = pg_load(ra, va, 64 * (q >> 1) + 16 * (q & 1));
+    }
+    bf16x8 xs[3];
+    x6_split(x[0], x[1], xs);
+    const bf16x8* lf = lw + (t * KB * 3) * 64 + lane;
+    bf16x8 fr[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) fr[0][p] = lf[p * 64];
+    f32x4 s[4], gL[4], a0[4];
+    int i = 0;
+    for (;;) {
+      const int r = plane_of(i);
+      int ni = i + 1;
+      int64_t nb = blk;
+      if (ni == R) {
+        ni = 0;
+        nb = blk + bstride;
+      }
+      const bool more = nb < nblk;
+      const Rsrc rn = win(g.A, KC, more ? nb : blk, plane_of(more ? ni : i));
+      const Rsrc ry = win(g.Y, NC, blk, r), rg = win(g.G, NC, blk, r);
+      const Rsrc rr = win(has_res ? g.res : g.Y, NC, blk, r);
+      const Rsrc ry0 = win(g.Y, NC, blk, 0);
+      // 0 value, 1 J, 3 L
+      const int kind = r == 0 ? 0 : r <= ndir ? 1 : 3;
+      f32x16 acc, accl, accm;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = accl[e] = accm[e] = 0.f;
+      f32x4 cb[4], yt[4];
+      pg_static_for<0, KB>([&](auto I) {
+        constexpr int kb = decltype(I)::value, cur = kb & 1, kn = (kb + 1) % KB;
+        if constexpr (kb == 0) {
+          if (i == 0) {   // block start: the previous layer's value plane (σ at KB / 2)
+#pragma unroll
+            for (int Q = 0; Q < 4; ++Q) s[Q] = pg_load(ry0, vc, (c0 + 8 * Q) * 4);
+          }
+        }
+        if constexpr (kb == KB / 2 - 1) {   // the plane's epilogue operands, half a plane ahead
+#pragma unroll
+          for (int Q = 0; Q < 4; ++Q) {
+            if (has_res) cb[Q] = pg_load(rr, vc, (c0 + 8 * Q) * 4);
+            if (kind != 0) yt[Q] = pg_load(ry, vc, (c0 + 8 * Q) * 4);
+          }
+        }
+        // next k block's fragments (past the plane's end: block 0 again) and terms (past the
+        // end: the next plane's block 0, loaded at this plane's block 0)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fr[cur ^ 1][p] = lf[(kn * 3 + p) * 64];
+        bf16x8 sn[3];
+        x6_split(x[2 * kn], x[2 * kn + 1], sn);
+        accl = x6_low(fr[cur], xs, accl);
+        accm = x6_mid(fr[cur], xs, accm);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[cur][0], xs[0], acc, 0, 0, 0);
+        // block kb was split one block ago: its registers take the next plane's
+        if (more) {
+          x[2 * kb] = pg_load(rn, va, 64 * kb);
+          x[2 * kb + 1] = pg_load(rn, va, 64 * kb + 16);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) xs[p] = sn[p];
+        if constexpr (kb == KB / 2) {
+          if (i == 0) {
+#pragma unroll
+            for (int Q = 0; Q < 4; ++Q) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) s[Q][e] = pa_sig10(s[Q][e]);
+              a0[Q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
+        }
+        if constexpr (kb == KB - 1) {
+#pragma unroll
+          for (int Q = 0; Q < 4; ++Q) {
+            f32x4 v = {acc[4 * Q], acc[4 * Q + 1], acc[4 * Q + 2], acc[4 * Q + 3]};
+            v += f32x4{accl[4 * Q], accl[4 * Q + 1], accl[4 * Q + 2], accl[4 * Q + 3]} +
+                 f32x4{accm[4 * Q], accm[4 * Q + 1], accm[4 * Q + 2], accm[4 * Q + 3]};
+            if (has_res) v += cb[Q];
+            const f32x4 sq = s[Q], ds = 10.f * sq * (1.f - sq);
+            f32x4 o;
+            if (kind == 3) {            // L_l: opens its group
+              gL[Q] = v;
+              o = v * sq;
+              a0[Q] += v * (yt[Q] * ds);
+            } else if (kind == 1) {     // J_k of the current group
+              const f32x4 J = yt[Q], dds = 10.f * ds * (1.f - 2.f * sq);
+              o = v * sq + 2.f * gL[Q] * J * ds;
+              a0[Q] += v * J * ds + gL[Q] * dds * (J * J);
+            } else {                    // value plane, last of the block
+              o = v * sq + a0[Q];
+              bsum[Q] += o;
+            }
+            pg_store(rg, o, vc, (c0 + 8 * Q) * 4);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      if (!more) break;
+      i = ni;
+      blk = nb;
+    }
+  }
+  // bias partials: the 32 points of each lane half summed in a fixed butterfly order
+#pragma unroll
+  for (int Q = 0; Q < 4; ++Q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = bsum[Q][e];
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      bsum[Q][e] = v;
+    }
+  if (j == 0) {   // row 2·wg + pb: the waves and the groups' workgroups fill disjoint columns
+#pragma unroll
+    for (int Q = 0; Q < 4; ++Q)
+      *reinterpret_cast<f32x4*>(g.partial + (2 * (int64_t)wg + pb) * NC + c0 + 8 * Q + 4 * h) =
+          bsum[Q];
+  }
+}
+
 // gbias[c] = Σ_b partial[b][c] in row order (deterministic); one thread per column
 __global__ void colsum_kernel(const float* __restrict__ partial, int nb, int nc,
                               float* __restrict__ out) {
@@ -1947,6 +2122,10 @@ bool wgrad_shape(int64_t M, int64_t N) {
 std::atomic<int> g_wgrad_mode{-1};
 int wgrad_mode() { return mode_from_env(g_wgrad_mode, "PNTF_GEMM_WGRAD", '2', 2); }
 bool wgrad_enabled() { return wgrad_mode() != 0; }
+// PNTF_GEMM_BWD: the kernel of pntf_tt_linear_bwd: 0 = panel_bwd_coop_kernel (fp32 MFMA), 1
+// (default) = panel_bwd_x6_kernel (split bf16)
+std::atomic<int> g_bwd_mode{-1};
+int bwd_mode() { return mode_from_env(g_bwd_mode, "PNTF_GEMM_BWD", '1', 1); }
 // Refill scheme per tile count: the two-buffer burst for the 256 x 256 gradients (T = 4:
 // 206 vs 215 µs at 9 x 20 000 rows), the per-slot ring for T = 1, 2 (64 vs 67, 103 vs 106 µs;
 // tools/wgrad_prof.sh).  PNTF_WGRAD_RING=1 or 2 forces one of them (to compare).
@@ -2012,6 +2191,12 @@ int pntf_tt_set_panel_mode(int mode) {
 int pntf_tt_set_wgrad_mode(int mode) {
   const int prev = wgrad_mode();
   if (mode >= 0 && mode <= 2) g_wgrad_mode = mode;
+  return prev;
+}
+
+int pntf_tt_set_bwd_mode(int mode) {
+  const int prev = bwd_mode();
+  if (mode >= 0 && mode <= 1) g_bwd_mode = mode;
   return prev;
 }
 
@@ -2335,7 +2520,9 @@ int pntf_tt_linear_act(int ndir, int nl, const float* x, int64_t m, int k, const
 }
 
 size_t pntf_tt_linear_bwd_work_floats(int kc, int nc) {
-  return (size_t)kc * nc + (size_t)num_cus() * nc;
+  // either kernel: the packed weight (fp32, or three bf16 terms = 1.5x) and the bias partials
+  // (one row per workgroup, or per point-block pair of a split-bf16 workgroup: <= 2 CUs + 16)
+  return (size_t)kc * nc * 3 / 2 + (2 * (size_t)num_cus() + 16) * nc;
 }
 
 int pntf_tt_linear_bwd(int ndir, int nl, const float* gy, int64_t m, int kc, const float* W,
@@ -2356,6 +2543,31 @@ int pntf_tt_linear_bwd(int ndir, int nl, const float* gy, int64_t m, int kc, con
     return PNTF_OK;
   }
   const int R = 1 + ndir + nl;
+  if (bwd_mode() == 1) {
+    const int64_t nf = (int64_t)(nc / 32) * (kc / 16) * 64;
+    hipLaunchKernelGGL(x6_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream,
+                       W, (int64_t)nc, 0, kc, nc, reinterpret_cast<bf16x8*>(work));
+    float* partial = work + (size_t)kc * nc * 3 / 2;
+    // one workgroup per CU (96 KiB of LDS), each on two 32-point blocks at a time; per 64-column
+    // group at most CUs / NG of them, a multiple of 8 so a block's group workgroups share an XCD
+    const int64_t pairs = ((m + 31) / 32 + 1) / 2, ng = nc / 64, cap = num_cus() / ng;
+    int64_t cw = pairs < cap ? pairs : cap;
+    cw = (cw + 7) / 8 * 8;
+    BwdArgs a{gy, reinterpret_cast<const f32x4*>(work), yprev, res, out, partial, m, R, ndir, nl};
+    const dim3 cg((unsigned)(cw * ng));
+    if (kc == 128 && nc == 128) hipLaunchKernelGGL((panel_bwd_x6_kernel<128, 128>), cg, dim3(256), 0, stream, a);
+    else if (kc == 128) hipLaunchKernelGGL((panel_bwd_x6_kernel<128, 256>), cg, dim3(256), 0, stream, a);
+    else if (nc == 128) hipLaunchKernelGGL((panel_bwd_x6_kernel<256, 128>), cg, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((panel_bwd_x6_kernel<256, 256>), cg, dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(colsum_kernel, dim3((nc + 255) / 256), dim3(256), 0, stream, partial,
+                       (int)(2 * cw), nc, gbias);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "pntf_tt_linear_bwd: %s", hipGetErrorString(e));
+      return PNTF_ERR_HIP;
+    }
+    return PNTF_OK;
+  }
   const int64_t nf = (int64_t)(nc / 32) * (kc / 8) * 64;
   hipLaunchKernelGGL(panel_pack_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0,
                      stream, W, (int64_t)nc, 0, kc, nc, reinterpret_cast<f32x4*>(work));

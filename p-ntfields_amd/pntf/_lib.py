@@ -110,6 +110,7 @@ SIGNATURES = {
     "pntf_tt_gemm_last_error": (ctypes.c_char_p, []),
     "pntf_tt_set_panel_mode": (ctypes.c_int, [ctypes.c_int]),
     "pntf_tt_set_wgrad_mode": (ctypes.c_int, [ctypes.c_int]),
+    "pntf_tt_set_bwd_mode": (ctypes.c_int, [ctypes.c_int]),
     "pntf_tt_linear_act": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_void_p, _i64, ctypes.c_int,
                                           _c_void_p, ctypes.c_int, _c_void_p, _c_void_p, _c_void_p,
                                           _c_void_p, ctypes.c_int, ctypes.c_int, _c_void_p,

@@ -3,7 +3,7 @@ the forward Linear + act (pntf_tt_linear_act: 0 AUTO, 1 fused one-wave-per-block
 act kernel, 3 fused four-waves-per-block), with and without the fused input gradient + act
 adjoint (pntf_tt_linear_bwd), at the reference batch 2 x 10 000 and 2 x 100 000.
 
-    python tools/train_sched_probe.py [reps]
+    python tools/train_sched_probe.py [reps [bwd]]   (bwd: only the input-gradient kernels)
 """
 import os
 import sys
@@ -16,7 +16,7 @@ import torch  # noqa: E402
 from pntf import synth, train  # noqa: E402
 
 
-def main(reps=10):
+def main(reps=10, only_bwd=False):
     from models import model_res_sigmoid_multi as md
     dev = torch.device("cuda:0")
     W = synth.make_weights(0)
@@ -37,9 +37,15 @@ def main(reps=10):
             opt.step()
             opt.zero_grad()
         defaults = (train._LINEAR_ACT, train._LINEAR_BWD)
-        for sched, bwd in (defaults, (0, 0), (2, 0), (1, 0), (3, 0), (3, 1), (2, 1), defaults):
+        runs = ((defaults + (1,)), (0, 0, 1), (2, 0, 1), (1, 0, 1), (3, 0, 1), (3, 1, 1),
+                (2, 1, 1), (defaults + (1,)))
+        if only_bwd:   # the fused input gradient + act adjoint: pair / split-bf16 / fp32 MFMA
+            runs = ((2, 0, 1), (2, 1, 1), (2, 1, 0), (2, 0, 1), (2, 1, 1), (2, 1, 0))
+        lib = train._lib.load()
+        for sched, bwd, bmode in runs:
             train._LINEAR_ACT = sched
             train._LINEAR_BWD = bwd
+            lib.pntf_tt_set_bwd_mode(bmode)
             step()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -47,9 +53,12 @@ def main(reps=10):
                 step()
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / reps * 1e3
-            print("train step %dx%d  linear_act schedule %d, fused bwd %s: %.3f ms"
-                  % (E, n, sched, "auto" if bwd is None else bwd, ms), flush=True)
+            print("train step %dx%d  linear_act schedule %d, fused bwd %s (bwd kernel %s): "
+                  "%.3f ms" % (E, n, sched, "auto" if bwd is None else bwd,
+                               "x6" if bmode else "fp32", ms), flush=True)
+        train._LINEAR_ACT, train._LINEAR_BWD = defaults
+        lib.pntf_tt_set_bwd_mode(1)
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10, len(sys.argv) > 2 and sys.argv[2] == "bwd")

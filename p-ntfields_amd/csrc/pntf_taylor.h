@@ -62,6 +62,13 @@ struct TaylorL {
 #ifndef PNTF_TAYLOR_X6
 #define PNTF_TAYLOR_X6 1
 #endif
+// 1: encoder[0] of the direction passes on split-bf16 as well, its J / L input rows built in TY
+// (round 6 experiment: C3 77.9 ms against 77.8-79.4 across boxes, componentwise Δτ error
+// 2.87e-4 against 2.55e-4, profiles/r06_c3_e0x6.txt: no measurable gain, so off); 0 (the
+// default): fp32 MFMA on the Fourier Jacobian rows computed per step
+#ifndef PNTF_TAYLOR_E0X6
+#define PNTF_TAYLOR_E0X6 0
+#endif
 // accumulate in the out bank, every out tile in one group (NX6_G = 16, pntf_common.h)
 #ifndef PNTF_TAYLOR_ACC
 #define PNTF_TAYLOR_ACC 1
@@ -247,6 +254,31 @@ __device__ __forceinline__ void taylor_direction(Rsrc W, const PairIO& io, int p
   for (int j = 0; j < DIM; ++j) xp[j] = p ? io.x[1][j] : io.x[0][j];
 
   // ---- encoder[0] on the Fourier Jacobian / Hessian rows (input_mapping_laplace :199-213)
+#if PNTF_TAYLOR_E0X6
+  // split-bf16 as the other layers: the J rows (js | jc) and L rows (ls | lc) of the 256
+  // Fourier features are the layer's two input columns, built in TY (free until encoder[-1])
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    f32x4 q = zero4(), wd = zero4();
+#pragma unroll
+    for (int j = 0; j < DIM; ++j) {
+      f32x4 wj = TWO_PI * ld4(io.Bw + j * H + 16 * kt + 4 * g);
+      q += xp[j] * wj;
+      wd = (j == d) ? wj : wd;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float sn, cs;
+      sincos_fast(q[s], sn, cs);
+      TY[kt][s] = wd[s] * cs;
+      TY[8 + kt][s] = -wd[s] * sn;
+      TY[16 + kt][s] = -wd[s] * wd[s] * sn;
+      TY[24 + kt][s] = -wd[s] * wd[s] * cs;
+    }
+  }
+  // + act_laplace of encoder[0] (:729), σ tiles T_E0 + 8p + ot
+  taylor_layer<8, 16, false, true>(W, F + OFF_E0 * 4, TY, TX, sc, T_E0 + p * 8, lane);
+#else
 #pragma unroll
   for (int i = 0; i < 16; ++i) TX[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
@@ -291,6 +323,7 @@ __device__ __forceinline__ void taylor_direction(Rsrc W, const PairIO& io, int p
     TX[ot] = gg * J;
     TX[8 + ot] = gp * J * J + gg * L;
   }
+#endif
 
   // ---- encoder residual blocks (:731-746)
 #pragma unroll 1
